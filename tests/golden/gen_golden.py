@@ -1,0 +1,421 @@
+"""Generate the golden vectors that pin the CPU oracle to the REFERENCE ITSELF.
+
+Runs only in the build container, where yaricom/Plastic-UNet is mounted read-only at
+/root/reference (it never travels to the GPU box).  It imports the reference's own ``src/unet``
+package (and, with stubs for the absent h5py/skimage/seaborn, ``src/train.py``'s ``train()``),
+runs it on seeded inputs and writes small ``.npz`` fixtures next to this file.  The fixtures are
+data (inputs + the reference's outputs); no reference source is stored.
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+Fixtures (each < 2 MB):
+  head_{hebb,oja}_N{32,128}.npz  plastic head fwd + BCE bwd (unet_p.py:69-88, train.py:101-110)
+  trace_seq_{hebb,oja}.npz       16 sequential head calls carrying the trace (train.py:88,99)
+  unetp_c8_{init,step,adam}.npz  reference-default UNetp at 64x64: init, fwd/bwd, 3 Adam+StepLR steps
+  unetp_d4c16_bs2_{init,out}.npz depth-4/base-16 trunk from the reference's own blocks, 2 slots
+  unetp_c64_sum.npz              depth-5/base-64 trunk (config C2 widths) at 32x32: outputs + grad sums
+  unetpres_n4.npz                UNetpRes(neurons=4) at 101x101, eval mode: params, fwd, grads
+  res_blocks.npz                 residual_block (relu-skip, S11) and res-up crop (S13)
+  bce_edge.npz                   BCELoss clamp edge cases (S9)
+  train_capture.npz              reference train() for 2 epochs (losses, eval, final params)
+  metrics.npz                    fast_iou_metric and RLE encode on fixed masks
+"""
+import os
+import sys
+import types
+import tempfile
+
+import numpy as np
+
+REF = "/root/reference/src"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+if not os.path.isdir(REF):
+    print("reference not present; nothing to generate")
+    sys.exit(0)
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+torch.set_num_threads(8)
+from unet import UNetp, UNetpRes  # noqa: E402  (the reference package)
+from unet import unet_p as ref_p  # noqa: E402
+from unet import unet_p_res as ref_r  # noqa: E402
+
+CPU = torch.device("cpu")
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print("wrote %-28s %7.1f KB" % (name, os.path.getsize(path) / 1024))
+
+
+def t2n(t):
+    return t.detach().cpu().numpy().copy()
+
+
+class _Pass(nn.Module):
+    def forward(self, a, b=None):
+        return a
+
+
+def head_only_net(rule, nbf):
+    """A reference UNetp whose trunk is bypassed so forward() runs only its plastic head."""
+    net = UNetp(1, 1, CPU, rule=rule, nbf=nbf)
+    for name in ["inc", "down1", "down2", "down3", "down4", "up1", "up2", "up3", "up4", "outc"]:
+        setattr(net, name, _Pass())
+    return net
+
+
+def gen_head():
+    for rule in ("hebb", "oja"):
+        for N in (32, 128):
+            g = torch.Generator().manual_seed(100 + N + (rule == "oja"))
+            net = head_only_net(rule, N)
+            with torch.no_grad():
+                net.w.copy_(0.05 * torch.randn(N, N, generator=g))
+                net.alpha.copy_(0.05 * torch.rand(N, N, generator=g))
+                net.eta.fill_(0.03)
+            X = (2.0 * torch.randn(N, N, generator=g))
+            H = 0.2 * torch.randn(N, N, generator=g)
+            t = (torch.rand(N, N, generator=g) > 0.5).float()
+            x = X.view(1, 1, N, N).clone().requires_grad_(True)
+            y, hn = net(x, H)
+            loss = nn.BCELoss()(y.view(-1), t.view(-1))
+            loss.backward()
+            save("head_%s_N%d.npz" % (rule, N), X=t2n(X), H=t2n(H), w=t2n(net.w), alpha=t2n(net.alpha),
+                 eta=t2n(net.eta), t=t2n(t), Y=t2n(y), Hn=t2n(hn), loss=t2n(loss),
+                 dX=t2n(x.grad.view(N, N)), dw=t2n(net.w.grad), dalpha=t2n(net.alpha.grad))
+
+
+def gen_trace_seq():
+    for rule in ("hebb", "oja"):
+        N = 32
+        g = torch.Generator().manual_seed(7 + (rule == "oja"))
+        net = head_only_net(rule, N)
+        with torch.no_grad():
+            net.w.copy_(0.1 * torch.randn(N, N, generator=g))
+            net.eta.fill_(0.05)
+        hebb = net.initialZeroHebb()
+        Xs, Ys, Hs = [], [], []
+        with torch.no_grad():
+            for _ in range(16):
+                X = 3.0 * torch.randn(N, N, generator=g)
+                y, hebb = net(X.view(1, 1, N, N), hebb)
+                Xs.append(t2n(X)); Ys.append(t2n(y)); Hs.append(t2n(hebb))
+        save("trace_seq_%s.npz" % rule, w=t2n(net.w), alpha=t2n(net.alpha), eta=t2n(net.eta),
+             X=np.stack(Xs), Y=np.stack(Ys), H=np.stack(Hs))
+
+
+def sd_arrays(module, prefix):
+    return {prefix + k: t2n(v) for k, v in module.state_dict().items()}
+
+
+def grad_arrays(module, prefix):
+    return {prefix + k: t2n(p.grad) for k, p in module.named_parameters() if p.grad is not None}
+
+
+def gen_unetp_c8():
+    """Reference default UNetp (unet_p.py, base 8, depth 5) at 64x64, driven like train.py:88-112."""
+    N = 64
+    torch.manual_seed(0)
+    net = UNetp(1, 1, CPU, rule="oja", nbf=N)
+    save("unetp_c8_init.npz", **sd_arrays(net, "p."))
+    g = torch.Generator().manual_seed(11)
+    xs = torch.rand(4, 1, 1, N, N, generator=g)
+    ts = (torch.rand(4, N, N, generator=g) > 0.5).float()
+    # single fwd/bwd with a non-zero trace
+    hebb0 = 0.1 * torch.randn(N, N, generator=g)
+    y, hn = net(xs[0], hebb0)
+    loss = nn.BCELoss()(y.view(-1), ts[0].view(-1))
+    loss.backward()
+    save("unetp_c8_step.npz", x=t2n(xs[0]), t=t2n(ts[0]), hebb=t2n(hebb0), Y=t2n(y), Hn=t2n(hn),
+         loss=t2n(loss), **grad_arrays(net, "g."))
+    # 3 steps of the train.py hot loop: Adam(lr) + StepLR(gamma .666, step 2) stepped per sample
+    net.zero_grad()
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    sch = torch.optim.lr_scheduler.StepLR(opt, gamma=0.666, step_size=2)
+    crit = nn.BCELoss()
+    hebb = net.initialZeroHebb()
+    losses = []
+    for k in range(1, 4):
+        opt.zero_grad()
+        y, hebb = net(xs[k], hebb.detach())
+        loss = crit(y.view(-1), ts[k].view(-1))
+        losses.append(loss.item())
+        loss.backward()
+        opt.step()
+        sch.step()
+    save("unetp_c8_adam.npz", xs=t2n(xs[1:]), ts=t2n(ts[1:]), losses=np.array(losses, np.float64),
+         hebb=t2n(hebb), **sd_arrays(net, "p."))
+
+
+def trunk_from_blocks(base, depth, nbf, rule, seed):
+    """UNetp assembled from the reference's OWN block classes with wider/shallower widths.
+
+    depth 4 uses the forward of unet_p.py:54-88 with down4 = identity and up1 = pass-through,
+    so x5 = x4 and the decoder starts at up2: the generalised depth-4 topology.
+    """
+    torch.manual_seed(seed)
+    net = UNetp(1, 1, CPU, rule=rule, nbf=nbf)
+    c = base
+    if depth == 5:
+        enc = [c, 2 * c, 4 * c, 8 * c, 8 * c]
+        net.inc = ref_p.inconv(1, enc[0], batch_norm=False)
+        net.down1 = ref_p.down(enc[0], enc[1], batch_norm=False)
+        net.down2 = ref_p.down(enc[1], enc[2], batch_norm=False)
+        net.down3 = ref_p.down(enc[2], enc[3], batch_norm=False)
+        net.down4 = ref_p.down(enc[3], enc[4], batch_norm=False)
+        net.up1 = ref_p.up(16 * c, 4 * c, batch_norm=False, bilinear=False)
+        net.up2 = ref_p.up(8 * c, 2 * c, batch_norm=False, bilinear=False)
+        net.up3 = ref_p.up(4 * c, c, batch_norm=False, bilinear=False)
+        net.up4 = ref_p.up(2 * c, c, batch_norm=False, bilinear=False)
+        names = ["inc", "down1", "down2", "down3", "down4", "up1", "up2", "up3", "up4", "outc"]
+        ours = names
+    else:
+        enc = [c, 2 * c, 4 * c, 4 * c]
+        net.inc = ref_p.inconv(1, enc[0], batch_norm=False)
+        net.down1 = ref_p.down(enc[0], enc[1], batch_norm=False)
+        net.down2 = ref_p.down(enc[1], enc[2], batch_norm=False)
+        net.down3 = ref_p.down(enc[2], enc[3], batch_norm=False)
+        net.down4 = _Pass()
+        net.up1 = _Pass()
+        net.up2 = ref_p.up(8 * c, 2 * c, batch_norm=False, bilinear=False)
+        net.up3 = ref_p.up(4 * c, c, batch_norm=False, bilinear=False)
+        net.up4 = ref_p.up(2 * c, c, batch_norm=False, bilinear=False)
+        names = ["inc", "down1", "down2", "down3", "up2", "up3", "up4", "outc"]
+        ours = ["inc", "down1", "down2", "down3", "up1", "up2", "up3", "outc"]
+    net.outc = ref_p.outconv(c, 1)
+    # deterministic re-init so the oracle can rebuild the same weights without storing them:
+    # parameter i (in the oracle's state_dict order) ~ U(-b, b), b = 1/sqrt(fan_in), seed 1000+i
+    order = ["w", "alpha", "eta"]
+    for nm, on in zip(names, ours):
+        for k in getattr(net, nm).state_dict().keys():
+            order.append((nm, on, k))
+    with torch.no_grad():
+        net.w.copy_(0.05 * torch.randn(nbf, nbf, generator=torch.Generator().manual_seed(seed + 1)))
+        net.alpha.copy_(0.05 * torch.rand(nbf, nbf, generator=torch.Generator().manual_seed(seed + 2)))
+        net.eta.fill_(0.02)
+        idx = 0
+        for item in order[3:]:
+            nm, on, k = item
+            p = getattr(net, nm).state_dict(keep_vars=True)[k]
+            fan = p.shape[1] * (p[0, 0].numel() if p.dim() > 1 else 1) if p.dim() > 1 else p.shape[0]
+            b = 1.0 / np.sqrt(max(fan, 1))
+            gg = torch.Generator().manual_seed(1000 + idx)
+            p.copy_((torch.rand(p.shape, generator=gg) * 2 - 1) * b)
+            idx += 1
+    return net, names, ours
+
+
+def gen_generalised():
+    # C1-shaped: depth 4, base 16, 128x128, two slots (each slot = one reference B=1 call)
+    N = 128
+    net, names, ours = trunk_from_blocks(16, 4, N, "hebb", seed=21)
+    arr = {}
+    for nm, on in zip(names, ours):
+        for k, v in getattr(net, nm).state_dict().items():
+            arr["p.%s.%s" % (on, k)] = t2n(v)
+    arr.update({"p.w": t2n(net.w), "p.alpha": t2n(net.alpha), "p.eta": t2n(net.eta)})
+    save("unetp_d4c16_bs2_init.npz", **arr)
+    g = torch.Generator().manual_seed(22)
+    x = torch.rand(2, 1, N, N, generator=g)
+    t = (torch.rand(2, N, N, generator=g) > 0.5).float()
+    H = 0.1 * torch.randn(2, N, N, generator=g)
+    Ys, Hs, losses = [], [], []
+    grads = {}
+    for b in range(2):
+        net.zero_grad()
+        y, hn = net(x[b:b + 1], H[b])
+        loss = nn.BCELoss()(y.view(-1), t[b].view(-1))
+        loss.backward()
+        Ys.append(t2n(y)); Hs.append(t2n(hn)); losses.append(loss.item())
+        for nm, on in zip(names, ours):
+            for k, p in getattr(net, nm).named_parameters():
+                grads.setdefault("g.%s.%s" % (on, k), []).append(t2n(p.grad))
+        for k in ("w", "alpha"):
+            grads.setdefault("g." + k, []).append(t2n(getattr(net, k).grad))
+    out = {k: np.mean(np.stack(v), 0) for k, v in grads.items()}   # batched = mean of slots
+    save("unetp_d4c16_bs2_out.npz", x=t2n(x), t=t2n(t), H=t2n(H), Y=np.stack(Ys), Hn=np.stack(Hs),
+         loss=np.float64(np.mean(losses)), **out)
+
+    # C2 widths (depth 5, base 64) at 32x32: outputs in full, gradients as checksums
+    N = 32
+    net, names, ours = trunk_from_blocks(64, 5, N, "oja", seed=31)
+    g = torch.Generator().manual_seed(32)
+    x = torch.rand(1, 1, N, N, generator=g)
+    t = (torch.rand(N, N, generator=g) > 0.5).float()
+    H = 0.1 * torch.randn(N, N, generator=g)
+    y, hn = net(x, H)
+    loss = nn.BCELoss()(y.view(-1), t.view(-1))
+    loss.backward()
+    arr = dict(x=t2n(x), t=t2n(t), H=t2n(H), Y=t2n(y), Hn=t2n(hn), loss=t2n(loss))
+    for nm, on in zip(names, ours):
+        for k, p in getattr(net, nm).named_parameters():
+            gnp = t2n(p.grad).astype(np.float64)
+            arr["gsum.%s.%s" % (on, k)] = np.array([gnp.sum(), np.abs(gnp).sum(), np.sqrt((gnp ** 2).sum())])
+            arr["ghead.%s.%s" % (on, k)] = t2n(p.grad).reshape(-1)[:16]
+            arr["psum.%s.%s" % (on, k)] = np.array([t2n(p).astype(np.float64).sum()])
+    for k in ("w", "alpha"):
+        gnp = t2n(getattr(net, k).grad).astype(np.float64)
+        arr["gsum." + k] = np.array([gnp.sum(), np.abs(gnp).sum(), np.sqrt((gnp ** 2).sum())])
+    save("unetp_c64_sum.npz", **arr)
+
+
+def gen_unetpres():
+    N = 101
+    torch.manual_seed(5)
+    net = UNetpRes(1, 1, CPU, neurons=4, rule="oja", nbf=N)
+    net.eval()     # S14: Dropout2d off
+    g = torch.Generator().manual_seed(6)
+    x = torch.rand(1, 1, N, N, generator=g)
+    t = (torch.rand(N, N, generator=g) > 0.5).float()
+    H = 0.1 * torch.randn(N, N, generator=g)
+    y, hn = net(x, H)
+    loss = nn.BCELoss()(y.view(-1), t.view(-1))
+    loss.backward()
+    save("unetpres_n4.npz", x=t2n(x), t=t2n(t), H=t2n(H), Y=t2n(y), Hn=t2n(hn), loss=t2n(loss),
+         **sd_arrays(net, "p."))
+    save("unetpres_n4_grad.npz", **grad_arrays(net, "g."))
+
+
+def gen_blocks():
+    torch.manual_seed(9)
+    rb = ref_r.residual_block(out_ch=6, batch_norm=False)
+    x = torch.randn(2, 6, 7, 7)
+    xin = x.clone()
+    yrb = rb(xin)          # note: mutates xin in place (S11)
+    up = ref_r.up(8, 4, dropout_ratio=0.0)
+    up.eval()
+    x1 = torch.randn(1, 8, 6, 6)
+    x2 = torch.randn(1, 4, 12, 12)
+    yup = up(x1, x2)
+    arr = {"rb_x": t2n(x), "rb_y": t2n(yrb), "up_x1": t2n(x1), "up_x2": t2n(x2), "up_y": t2n(yup)}
+    arr.update(sd_arrays(rb, "rb."))
+    arr.update(sd_arrays(up, "up."))
+    save("res_blocks.npz", **arr)
+
+
+def gen_bce():
+    y = torch.tensor([0.0, 1e-30, 1e-8, 0.3, 0.5, 0.7, 1 - 1e-7, 1.0, 1.0, 0.0, 0.2, 0.9999],
+                     dtype=torch.float32).requires_grad_(True)
+    t = torch.tensor([0.0, 0.0, 1.0, 1.0, 0.0, 0.5, 1.0, 0.0, 1.0, 1.0, 0.3, 0.0], dtype=torch.float32)
+    loss = nn.BCELoss()(y, t)
+    loss.backward()
+    # logits that saturate the fp32 sigmoid to exactly 1.0 (S9)
+    z = torch.tensor([15.0, 16.0, 16.7, 17.0, 20.0, -20.0, -104.0, -110.0], requires_grad=True)
+    tz = torch.tensor([0.0, 0.0, 0.0, 0.0, 0.0, 1.0, 1.0, 1.0])
+    yz = torch.sigmoid(z)
+    lz = nn.BCELoss()(yz, tz)
+    lz.backward()
+    save("bce_edge.npz", y=t2n(y), t=t2n(t), loss=t2n(loss), dy=t2n(y.grad), z=t2n(z), tz=t2n(tz),
+         yz=t2n(yz), lz=t2n(lz), dz=t2n(z.grad))
+
+
+CAPTURED = {}
+
+
+def install_stubs():
+    """Stand-ins for the absent h5py/skimage/seaborn so the reference's utils/train import."""
+    captured = CAPTURED
+
+    class _F:
+        def __init__(self, *a, **k):
+            pass
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+        def create_dataset(self, name, data=None, **kw):
+            captured[name] = np.array(data)
+
+        def flush(self):
+            pass
+
+    h5 = types.ModuleType("h5py"); h5.File = _F
+    sk = types.ModuleType("skimage"); sk.io = types.ModuleType("skimage.io")
+    sk.transform = types.ModuleType("skimage.transform")
+    sk.io.imread = sk.io.imsave = lambda *a, **k: None
+    sk.transform.resize = lambda *a, **k: None
+    sns = types.ModuleType("seaborn")
+    sns.__getattr__ = lambda name: (lambda *a, **k: None)
+    # matplotlib is installed but lacks the 'seaborn-white' style the reference selects at import
+    mpl = types.ModuleType("matplotlib"); plt = types.ModuleType("matplotlib.pyplot")
+    plt.__getattr__ = lambda name: (lambda *a, **k: None)
+    plt.style = types.SimpleNamespace(use=lambda *a, **k: None)
+    mpl.pyplot = plt
+    for name, mod in [("h5py", h5), ("skimage", sk), ("skimage.io", sk.io),
+                      ("skimage.transform", sk.transform), ("seaborn", sns),
+                      ("matplotlib", mpl), ("matplotlib.pyplot", plt)]:
+        sys.modules.setdefault(name, mod)
+
+
+def gen_train_capture():
+    """Reference ``train()`` (train.py:29-211) on synthetic data with h5py/skimage/seaborn stubbed."""
+    install_stubs()
+    captured = CAPTURED
+    import train as ref_train  # noqa: E402  (reference src/train.py)
+
+    N = 32
+    torch.manual_seed(3)
+    net = UNetp(1, 1, CPU, rule="oja", nbf=N)
+    init = sd_arrays(net, "init.")
+    g = np.random.RandomState(4)
+    X_train = g.rand(3, 1, N, N).astype(np.float32)
+    y_train = (g.rand(3, 1, N, N) > 0.5).astype(np.float32)
+    X_val = g.rand(1, 1, N, N).astype(np.float32)
+    y_val = (g.rand(1, 1, N, N) > 0.5).astype(np.float32)
+    with tempfile.TemporaryDirectory() as d:
+        params = {"out_dir": d, "device": CPU, "epochs": 2, "stop_time": -1, "lr": 3e-4,
+                  "val_ratio": 0.05, "val_every": 1, "save_every": 1, "rollout": 100, "gamma": 0.666,
+                  "steplr": 4, "prule": "oja", "im_width": N, "im_height": N, "im_chan": 1,
+                  "debug": False}
+        ref_train.train(net, X_train, X_val, y_train, y_val, params)
+    arr = dict(X_train=X_train, y_train=y_train, X_val=X_val, y_val=y_val,
+               all_losses=captured["train/all_losses"],
+               val_train_losses=captured["validation/train_losses"],
+               val_test_losses=captured["validation/test_losses"],
+               val_accuracies=captured["validation/accuracies"])
+    arr.update(init)
+    arr.update(sd_arrays(net, "final."))
+    save("train_capture.npz", **arr)
+
+
+def gen_metrics():
+    import importlib.util
+
+    def load(path, name):
+        spec = importlib.util.spec_from_file_location(name, os.path.join(REF, path))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+    fast_iou_metric = load("utils/iou_metric.py", "ref_iou_metric").fast_iou_metric
+    encode = load("utils/rle_encode.py", "ref_rle_encode").encode
+    g = np.random.RandomState(12)
+    yt = (g.rand(3, 101 * 101) > 0.6).astype(np.float32).reshape(-1)
+    yp = g.rand(3 * 101 * 101).astype(np.float32)
+    iou = fast_iou_metric(y_true_in=yt, y_pred_in=yp)
+    masks = (g.rand(4, 101, 101) > 0.7)
+    masks[0] = False
+    masks[1] = True
+    rles = [encode(np.round(m)) for m in masks]
+    save("metrics.npz", yt=yt, yp=yp, iou=np.float64(iou), masks=masks,
+         rles=np.array(rles, dtype=object).astype(str))
+
+
+if __name__ == "__main__":
+    gen_head()
+    gen_trace_seq()
+    gen_unetp_c8()
+    gen_generalised()
+    gen_unetpres()
+    gen_blocks()
+    gen_bce()
+    gen_metrics()
+    gen_train_capture()
