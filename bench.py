@@ -1,0 +1,244 @@
+"""Headline benchmark: training images/sec of the plastic U-Net (BASELINE.json metric), MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload = config C2 (BASELINE.json configs[1]): UNetp depth 5 / base 64 (14.81 M params), Oja
+rule, 1x128x128 synthetic tiles, batch 32 per GPU, fp32.  A step = forward + BCE + backward
+(+ RCCL gradient all-reduce when N > 1) + Adam + StepLR over one resident batch, with the per-slot
+plastic traces carried step to step.  Timed region: barrier + synchronize on both sides, max over
+ranks; value = images of all ranks / time (weak scaling: 32 images per GPU).
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+  roofline      the dominant kernel's algorithmic TFLOP/s vs the fp32 MFMA peak, from HIP events
+                bracketing each launch on its own stream during a separate instrumented pass
+  kernels       per-kernel-instantiation time/FLOP breakdown of one step
+  oja_update    the Oja trace update's algorithmic GB/s (bs x 128^2, cache-resident) and an
+                HBM-sized sweep (8192 traces, 1 GiB per pass)
+  cpu_baseline  the CPU oracle (oracle/ref_cpu.py, fixture-pinned restatement of the reference)
+                in the reference's own mode (bs=1, Adam per sample) on the host cores, N=1 only
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "plastic-unet_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--img", type=int, default=128)
+    ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--base", type=int, default=64)
+    ap.add_argument("--rule", default="oja")
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--steplr", type=float, default=1e5)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-profile", action="store_true")
+    return ap.parse_args()
+
+
+def fp32_mfma_peak_tflops(kernels):
+    cu, clk_khz, _ = kernels.device_info(torch.cuda.current_device())
+    # v_mfma_f32_32x32x2_f32: 64 FLOP/clk/SIMD x 4 SIMDs per CU (MI355X_MICROARCH.md)
+    clk_ghz = clk_khz / 1e6 if clk_khz > 0 else 2.4
+    return 256.0 * cu * clk_ghz / 1e3, cu, clk_ghz
+
+
+def cpu_baseline(args):
+    """The oracle's reference-mode training loop on the host cores: bs=1, Adam per sample."""
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    net = oracle.RefUNetp(1, 1, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base)
+    opt = oracle.ref_adam(net.parameters(), args.lr)
+    sch = oracle.ref_steplr(opt, int(args.steplr))
+    g = torch.Generator().manual_seed(4321)
+    xs = torch.rand(4, 1, 1, args.img, args.img, generator=g)
+    ts = (torch.rand(4, args.img, args.img, generator=g) > 0.5).float()
+    hebb = net.initialZeroHebb()
+    oracle.ref_train_step(net, opt, sch, xs[0], ts[0], hebb)          # warm-up sample
+    n, t0 = 0, time.perf_counter()
+    while True:
+        _, _, hebb = oracle.ref_train_step(net, opt, sch, xs[n % 4], ts[n % 4], hebb)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= args.cpu_seconds and n >= 2) or n >= 200:
+            break
+    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": "oracle/ref_cpu.py RefUNetp depth %d base %d %dx%d, reference mode (bs=1, fwd+BCE+bwd+Adam "
+                      "per sample, train.py:91-112): %d samples in %.1f s on %d threads"
+                      % (args.depth, args.base, args.img, args.img, n, el, threads)}
+
+
+def oja_update_bench(K, B, N, device):
+    """Algorithmic GB/s of the trace update: 8*B*N^2 + 8*B*N bytes (read H, write H', rows)."""
+    res = {}
+    eta = torch.full((1,), 0.01, device=device)
+    for label, bb, reps in (("bs%d" % B, B, 200), ("hbm_sweep_8192", 8192, 20)):
+        H = torch.randn(bb, N, N, device=device)
+        X = torch.randn(bb, N, N, device=device)
+        Y = torch.rand(bb, N, N, device=device)
+        out = torch.empty_like(H)
+        for _ in range(3):
+            K.trace_update(H, X, Y, eta, 1, out=out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            K.trace_update(H, X, Y, eta, 1, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        nbytes = 8.0 * bb * N * N + 8.0 * bb * N
+        res[label] = {"us_per_launch": round(us, 3), "bytes": nbytes, "GB_s": round(nbytes / us / 1e3, 1)}
+        del H, X, Y, out
+    return res
+
+
+def main():
+    args = parse()
+    from punet import dp
+    world, rank, local = dp.init_from_env("nccl")
+    if world != args.gpus and rank == 0:
+        print("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+
+    from unet import UNetp
+    from punet import kernels as K
+    from punet.engine import Trainer
+
+    torch.manual_seed(0)
+    net = UNetp(1, 1, device, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base)
+    dp.broadcast_params(net)
+    trainer = Trainer(net, lr=args.lr, steplr=args.steplr)
+
+    B, S = args.batch, args.img
+    g = torch.Generator().manual_seed(1234 + rank)
+    NB = 4  # distinct synthetic batches resident in HBM, cycled
+    xs = [torch.rand(B, 1, S, S, generator=g).to(device) for _ in range(NB)]
+    ts = [(torch.rand(B, S, S, generator=g) > 0.5).float().to(device) for _ in range(NB)]
+    hebb = net.initialZeroHebb(B)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    loss = None
+    for i in range(args.warmup):
+        loss, hebb = trainer.step(xs[i % NB], ts[i % NB], hebb)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss, hebb = trainer.step(xs[i % NB], ts[i % NB], hebb)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    final_loss = loss.item() if loss is not None else float("nan")
+
+    # ---------------- instrumented pass: per-launch HIP events on the launching stream
+    kern = None
+    roof = None
+    if not args.no_kernel_profile:
+        nprof = max(1, min(3, args.steps))
+        with K.KernelProfiler() as prof:
+            for i in range(nprof):
+                loss, hebb = trainer.step(xs[i % NB], ts[i % NB], hebb)
+        summ = prof.summary()
+        kern = {}
+        for tag, d in sorted(summ.items(), key=lambda kv: -kv[1]["ms"]):
+            e = {"launches_per_step": d["launches"] / nprof, "ms_per_step": round(d["ms"] / nprof, 4)}
+            if d["flops"]:
+                e["TFLOP_s"] = round(d["flops"] / (d["ms"] * 1e-3) / 1e12, 2)
+            if d["bytes"]:
+                e["GB_s"] = round(d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1)
+            kern[tag] = e
+        peak, cu, clk = fp32_mfma_peak_tflops(K)
+        mfma = {t: d for t, d in summ.items() if d["flops"] and (t.startswith("igemm") or t.startswith("wgrad"))}
+        dom = max(mfma.items(), key=lambda kv: kv[1]["ms"])
+        dtag, dd = dom
+        ach = dd["flops"] / (dd["ms"] * 1e-3) / 1e12
+        tot_f = sum(d["flops"] for d in mfma.values())
+        tot_ms = sum(d["ms"] for d in mfma.values())
+        roof = {"kernel": dtag, "bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
+                "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                "launches_per_step": dd["launches"] / nprof,
+                "avg_launch_us": round(dd["ms"] * 1e3 / dd["launches"], 2),
+                "algorithmic_flop_per_launch": dd["flops"] / dd["launches"],
+                "all_conv_mfma": {"achieved": round(tot_f / (tot_ms * 1e-3) / 1e12, 2),
+                                  "frac": round(tot_f / (tot_ms * 1e-3) / 1e12 / peak, 4),
+                                  "flop_per_step": tot_f / nprof, "ms_per_step": round(tot_ms / nprof, 3)},
+                "peak_basis": "fp32 MFMA 256 FLOP/clk/CU x %d CU x %.2f GHz" % (cu, clk)}
+        prof_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(prof_path):
+            try:
+                tr = json.load(open(prof_path)).get(dtag)
+                if tr:
+                    roof["traffic"] = tr.get("hbm_bytes_per_launch")
+            except Exception:
+                pass
+
+    oja = None
+    if rank == 0:
+        oja = oja_update_bench(K, B, S, device)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        value = world * B * args.steps / elapsed
+        line = {
+            "metric": "training images/sec (128x128, bs=32 per GPU)",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: x~U[0,1) [B,1,%d,%d], targets (U>0.5); random init (seed 0)" % (S, S),
+            "config": {"workload": "C2: UNetp depth %d base_ch %d, %s rule, 1x%dx%d, fwd+BCE+bwd+Adam"
+                                   % (args.depth, args.base, args.rule, S, S),
+                       "global_batch": world * B, "per_gpu_batch": B, "img": S,
+                       "parallelism": "dp%d" % world if world > 1 else "single"},
+            "final_loss": final_loss,
+            "roofline": roof,
+            "oja_update": oja,
+            "cpu_baseline": cpu,
+            "kernels": kern,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

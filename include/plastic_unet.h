@@ -1,0 +1,231 @@
+/*
+ * plastic_unet.h - C-ABI of libplastic_unet.so, the MI355X (gfx950) kernels of the plastic U-Net
+ * training path.  Plain pointers and sizes only; no torch/HIP types in any signature.
+ *
+ * The reference (yaricom/Plastic-UNet) is pure Python: its "interface" for this path is the set of
+ * ATen operators its nn.Modules call.  Each entry point below names the reference call site(s) it
+ * replaces (paths relative to the reference repo):
+ *
+ *   pu_conv_igemm      nn.Conv2d(k=3,p=1)+ReLU fwd     src/unet/unet_p.py:184-201 (double_conv)
+ *                      conv3x3 backward-data           (autograd of the same, train.py:110)
+ *                      nn.ConvTranspose2d(2,s=2) fwd   src/unet/unet_p.py:238 (up.up)
+ *                      ConvTranspose2d backward-data   (autograd, train.py:110)
+ *                      torch.cat([x2,x1],1) (fused)    src/unet/unet_p.py:248
+ *   pu_wgrad           conv3x3 / ConvT weight+bias gradients (autograd, train.py:110)
+ *   pu_maxpool2_fwd    nn.MaxPool2d(2)                 src/unet/unet_p.py:222 (down.mpconv)
+ *   pu_maxpool2_bwd    its backward (+ the ReLU mask of the pooled tensor)
+ *   pu_outconv_fwd/bwd nn.Conv2d(C,1,1) (outconv)      src/unet/unet_p.py:253-260
+ *   pu_plastic_fwd     activin.mm(w+alpha*hebb), sigmoid, Hebb/Oja trace update
+ *                                                      src/unet/unet_p.py:69-88
+ *   pu_trace_update    the trace update alone          src/unet/unet_p.py:81-86
+ *   pu_plastic_bwd     mm/mul/sigmoid backward         (autograd, train.py:110)
+ *   pu_bce_fwd/bwd     nn.BCELoss (mean, log >= -100)  src/train.py:70,101-105
+ *   pu_adam_multi      torch.optim.Adam.step           src/train.py:66,111
+ *   pu_pack_weight     (layout only) OIHW parameters -> the packed GEMM operands
+ *   pu_nchw_to_nhwc    (layout only) the [B,C,H,W] model input -> NHWC
+ *
+ * Conventions
+ *   - Activations are NHWC fp32 in device memory (HBM).  Parameters keep PyTorch's layout (OIHW,
+ *     ConvT [in][out][kh][kw]) so state_dicts load both ways; pu_pack_weight makes GEMM operands.
+ *   - Ownership: the caller owns every buffer.  The library never allocates or frees device
+ *     memory; scratch is passed in as `workspace` (size from the *_workspace_bytes query).
+ *   - Streams: `stream` is a hipStream_t (NULL = default stream).  Every call only enqueues work
+ *     on that stream; none synchronises, so calls are hipGraph-capturable.
+ *   - Errors: 0 on success, a negative pu_status otherwise; pu_last_error() returns a
+ *     thread-local message for the last failing call on this thread.
+ *   - Threading: stateless and re-entrant; safe from several host threads on different streams.
+ */
+#ifndef PLASTIC_UNET_H
+#define PLASTIC_UNET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PU_ABI_VERSION 1
+
+typedef enum {
+    PU_OK = 0,
+    PU_ERR_INVALID = -1,     /* bad argument (shape, null pointer, alignment) */
+    PU_ERR_UNSUPPORTED = -2, /* valid but not implemented for this shape */
+    PU_ERR_LAUNCH = -3,      /* HIP launch error */
+    PU_ERR_WORKSPACE = -4    /* workspace too small */
+} pu_status;
+
+int pu_abi_version(void);
+const char* pu_last_error(void);
+/* number of compute units and shader clock (kHz) of `device` (for roofline peaks) */
+int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes);
+
+/* ---------------------------------------------------------------------------------------------
+ * Implicit-GEMM convolution on MFMA (v_mfma_f32_32x32x2_f32):  D[m][n] = sum_k A[m][k] W[n][k]
+ *   rows m  = output pixels (batch, out_h, out_w) of the GEMM grid
+ *   cols k  = (tap r*kw+s, channel c) of the input at pixel (ho*stride-pad+r, wo*stride-pad+s),
+ *             channels [0,c0) read from src0 and [c0,c0+c1) from src1 (concat without a copy)
+ *   weight  = packed [n][k_pad] (pu_pack_weight), k_pad >= kh*kw*(c0+c1), k_pad % 16 == 0
+ * Epilogue per element: v = acc (+ bias) ; RELU: v = max(v,0) ; mask: v *= (mask > 0) ;
+ *   ACCUM: dst += v else dst = v.  Columns [0,n0) go to dst0 (NHWC, n0 channels), [n0,n) to
+ *   dst1 (NHWC, n-n0 channels).  SHUFFLE2: n = (2i+j)*co + c is stored at pixel (2ho+i, 2wo+j)
+ *   of a (2*out_h, 2*out_w) NHWC grid with co = n/4 channels and bias[c] (ConvTranspose2d 2x2 s2).
+ * ------------------------------------------------------------------------------------------- */
+enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4 };
+
+typedef struct {
+    int batch;
+    int in_h, in_w;
+    int out_h, out_w;
+    int kh, kw, stride, pad;
+    const float* src0; int c0;
+    const float* src1; int c1;
+    const float* weight; int k_pad;
+    int n;
+    const float* bias;
+    float* dst0; int n0;
+    float* dst1;
+    const float* mask0;
+    const float* mask1;
+    int flags;
+} pu_conv_args;
+
+int pu_conv_igemm(const pu_conv_args* a, void* stream);
+/* the kernel instantiation pu_conv_igemm would launch: block tile bm x bn and A-loader mode
+ * (0 = 16-channel chunks, 1 = float4, 2 = scalar); for profiling/roofline attribution */
+int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* mode);
+
+/* ---------------------------------------------------------------------------------------------
+ * Weight/bias gradient of a convolution as a split-K MFMA GEMM over the B*H*W pixel rows:
+ *   dweight[n][c][r][s] = sum_m P[m][n] * X[pix(m,r,s)][c]          (+ accumulate)
+ *   P = rows operand [batch*out_h*out_w][n] (conv: dZ;  ConvT: its low-res input x)
+ *   X = im2col operand at the (in_h,in_w) grid, channels from src0/src1 as in pu_conv_igemm
+ *       (conv: the layer input; ConvT: the high-res output gradient)
+ *   bias_mode 1: dbias[n] = sum_m P[m][n]                      (conv bias)
+ *   bias_mode 2: dbias[c] = sum_m sum_(r,s) X[pix(m,r,s)][c]   (ConvT bias)
+ * Output layout [n][c][kh][kw] is PyTorch's: conv OIHW (n=out, c=in), ConvT [in][out][kh][kw].
+ * Deterministic: per-split partials go to `workspace`, then a fixed-order reduction.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    int batch;
+    int in_h, in_w;
+    int out_h, out_w;
+    int kh, kw, stride, pad;
+    const float* rows; int n;
+    const float* src0; int c0;
+    const float* src1; int c1;
+    int bias_mode;
+    float* dweight;
+    float* dbias;
+    int accumulate;
+} pu_wgrad_args;
+
+size_t pu_wgrad_workspace_bytes(const pu_wgrad_args* a);
+/* the tile (bn x bk), loader (qvec) and pixel-row split count pu_wgrad would use */
+int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec, int* splits);
+int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Layout helpers
+ * ------------------------------------------------------------------------------------------- */
+enum {
+    PU_PACK_CONV_FWD = 0,   /* w[O][I][R][S] -> p[o][(r*S+s)*I+i]                          */
+    PU_PACK_CONV_DGRAD = 1, /* w[O][I][R][S] -> p[i][((R-1-r)*S+(S-1-s))*O+o] (flipped)    */
+    PU_PACK_CONVT_FWD = 2,  /* w[I][O][R][S] -> p[(r*S+s)*O+o][i]                           */
+    PU_PACK_CONVT_DGRAD = 3 /* w[I][O][R][S] -> p[i][(r*S+s)*O+o]                           */
+};
+/* d0,d1 = first two dims of w; rows of p are k_pad floats wide (zero padded) */
+int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw,
+                   int k_pad, void* stream);
+int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, void* stream);
+
+/* MaxPool2d(2) on NHWC (floor for odd sizes), first-max tie rule of ATen's CPU kernel.
+ * bwd: dx[argmax] (+)= dy * (relu_mask ? (x[argmax] > 0) : 1); dx elsewhere: 0 (or kept if
+ * accumulate). */
+int pu_maxpool2_fwd(const float* x, float* y, int batch, int h, int w, int c, void* stream);
+int pu_maxpool2_bwd(const float* x, const float* dy, float* dx, int batch, int h, int w, int c,
+                    int relu_mask, int accumulate, void* stream);
+
+/* outconv (1x1, C -> 1): y[m] = b + sum_c x[m][c]*w[c].
+ * bwd: dx[m][c] = dy[m]*w[c]*(relu_mask ? x[m][c] > 0 : 1); dw[c] = sum_m dy[m]x[m][c];
+ *      db = sum_m dy[m]  (workspace: pu_outconv_workspace_bytes) */
+int pu_outconv_fwd(const float* x, const float* w, const float* b, float* y, long long rows, int c,
+                   void* stream);
+size_t pu_outconv_workspace_bytes(long long rows, int c);
+int pu_outconv_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db,
+                   long long rows, int c, int relu_mask, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Plastic head (unet_p.py:69-88), batched over per-slot traces:
+ *   Y_b = sigmoid(X_b (w + alpha (.) H_b))
+ *   hebb rule (0): H'_b = (1-eta) H_b + eta x0 y0^T ;  oja rule (1): H'_b = H_b + eta (x0 - H_b y0) y0
+ *   with x0 = X_b[0,:], y0 = Y_b[0,:]; hebb_out may be NULL (eval: trace not updated).
+ * eta is a device pointer (the learnable parameter).
+ * ------------------------------------------------------------------------------------------- */
+enum { PU_RULE_HEBB = 0, PU_RULE_OJA = 1 };
+
+typedef struct {
+    int batch, nbf;
+    const float* x;
+    const float* hebb;
+    const float* w;
+    const float* alpha;
+    const float* eta;
+    float* y;
+    float* hebb_out;
+    int rule;
+} pu_plastic_args;
+
+int pu_plastic_fwd(const pu_plastic_args* a, void* stream);
+int pu_trace_update(const float* hebb, const float* x, const float* y, const float* eta,
+                    float* hebb_out, int batch, int nbf, int rule, void* stream);
+
+/* backward given dy = dL/dY:  G = dy*(1-y)*y ; dx_b = G_b Weff_b^T ;
+ *   dw = sum_b X_b^T G_b ; dalpha = sum_b (X_b^T G_b) (.) H_b   (no gradient to eta: S3) */
+typedef struct {
+    int batch, nbf;
+    const float* x;
+    const float* hebb;
+    const float* w;
+    const float* alpha;
+    const float* y;
+    const float* dy;
+    float* dx;
+    float* dw;
+    float* dalpha;
+} pu_plastic_bwd_args;
+
+size_t pu_plastic_bwd_workspace_bytes(int batch, int nbf);
+int pu_plastic_bwd(const pu_plastic_bwd_args* a, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
+/* BCELoss (mean): loss = mean((t-1)*max(log1p(-y),-100) - t*max(log(y),-100))
+ * bwd: dy = g * (y-t) / max((1-y)*y, 1e-12) / n, g = *grad_loss (device scalar) */
+size_t pu_bce_workspace_bytes(long long n);
+int pu_bce_fwd(const float* y, const float* t, long long n, float* loss, void* workspace,
+               size_t workspace_bytes, void* stream);
+int pu_bce_bwd(const float* y, const float* t, long long n, const float* grad_loss, float* dy,
+               void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Multi-tensor Adam (torch.optim.Adam, amsgrad=False, maximize=False):
+ *   m = lerp(m, g, 1-beta1) ; v = v*beta2 + (1-beta2) g^2 ;
+ *   p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)      (weight_decay adds wd*p to g first)
+ * step_size = lr/(1-beta1^t) and bc2_sqrt = sqrt(1-beta2^t) are computed by the caller.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    long long numel;
+} pu_adam_tensor;
+
+int pu_adam_multi(const pu_adam_tensor* tensors, int n_tensors, float beta1, float beta2, float eps,
+                  float weight_decay, float step_size, float bc2_sqrt, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLASTIC_UNET_H */

@@ -1,0 +1,69 @@
+// Shared helpers of libplastic_unet.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "plastic_unet.h"
+
+namespace pu {
+
+// ------------------------------------------------------------------------------ error reporting
+extern thread_local char g_last_error[512];
+
+inline int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(PU_ERR_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+    return PU_OK;
+}
+
+#define PU_REQUIRE(cond, ...)                                          \
+    do {                                                               \
+        if (!(cond)) return ::pu::fail(PU_ERR_INVALID, __VA_ARGS__);   \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ----------------------------------------------------------- integer division by a runtime divisor
+// q = umulhi(x, mul) >> shift  for 0 <= x < 2^31, d >= 1 (Granlund-Montgomery round-up method)
+struct FastDiv {
+    uint32_t d, mul, shift;
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    if (d == 1) {
+        f.mul = 0;
+        f.shift = 0;
+        return f;
+    }
+    uint32_t l = 0;
+    while ((1u << l) < d) ++l;
+    // mul = ceil(2^(32+l) / d) - 2^32 ... use the simpler 64-bit form
+    uint64_t m = ((uint64_t(1) << (32 + l)) + d - 1) / d;
+    f.mul = uint32_t(m);  // m < 2^33; keep the low 32 bits, add x back (see div())
+    f.shift = l;
+    return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+    if (f.d == 1) return x;
+    // q = (x + umulhi(x, mul_lo)) >> l  where mul = 2^32 + mul_lo ;  x < 2^31 so no overflow
+    uint32_t hi = __umulhi(x, f.mul);
+    return (hi + x) >> f.shift;
+}
+
+inline int ceil_div(long long a, long long b) { return int((a + b - 1) / b); }
+
+}  // namespace pu

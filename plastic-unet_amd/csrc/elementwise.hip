@@ -1,0 +1,349 @@
+// Bandwidth-bound kernels of the trunk: parameter packing, NCHW->NHWC input, MaxPool2d(2)
+// forward/backward and the 1x1 outconv (C -> 1) forward/backward.  All HBM-bound: float4 (16 B
+// per lane) accesses along the contiguous NHWC channel axis.
+//
+// Reference call sites (yaricom/Plastic-UNet): nn.MaxPool2d(2) in down (src/unet/unet_p.py:222),
+// outconv nn.Conv2d(C, n_classes, 1) (unet_p.py:253-260), and their autograd backward
+// (src/train.py:110).
+#include "common.h"
+
+#include <math.h>
+
+namespace pu {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void pack_weight_kernel(const float* __restrict__ w, float* __restrict__ p, int mode, int d0, int d1,
+                                   int kh, int kw, int k_pad, int rows) {
+    const long long total = (long long)rows * k_pad;
+    const int taps = kh * kw;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int row = int(idx / k_pad);
+        const int k = int(idx - (long long)row * k_pad);
+        float v = 0.f;
+        if (mode == PU_PACK_CONV_FWD) {          // w[O=d0][I=d1][R][S] -> [o][(r*S+s)*I+i]
+            if (k < taps * d1) {
+                int tap = k / d1, i = k - tap * d1;
+                v = w[((long long)row * d1 + i) * taps + tap];
+            }
+        } else if (mode == PU_PACK_CONV_DGRAD) { // -> [i][((R-1-r)*S+(S-1-s))*O+o]
+            if (k < taps * d0) {
+                int tapf = k / d0, o = k - tapf * d0;
+                int tap = taps - 1 - tapf;       // (R-1-r, S-1-s) flattened == taps-1-(r*S+s)
+                v = w[((long long)o * d1 + row) * taps + tap];
+            }
+        } else if (mode == PU_PACK_CONVT_FWD) {  // w[I=d0][O=d1][R][S] -> [(r*S+s)*O+o][i]
+            if (k < d0) {
+                int tap = row / d1, o = row - tap * d1;
+                v = w[((long long)k * d1 + o) * taps + tap];
+            }
+        } else {                                 // PU_PACK_CONVT_DGRAD: -> [i][(r*S+s)*O+o]
+            if (k < taps * d1) {
+                int tap = k / d1, o = k - tap * d1;
+                v = w[((long long)row * d1 + o) * taps + tap];
+            }
+        }
+        p[idx] = v;
+    }
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ s, float* __restrict__ d, int C, int HW, long long total) {
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int c = int(idx % C);
+        const long long bp = idx / C;
+        const long long b = bp / HW;
+        const int pix = int(bp - b * HW);
+        d[idx] = s[(b * C + c) * HW + pix];
+    }
+}
+
+// ATen CPU max-pool rule: scan the window row-major, take val if (val > max || isnan(val)).
+__device__ __forceinline__ void pool_take(float v, int idx, float& best, int& arg) {
+    if (v > best || isnan(v)) {
+        best = v;
+        arg = idx;
+    }
+}
+
+template <bool VEC>
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int H, int W, int C, int Ho,
+                                   int Wo, long long total) {
+    const int CV = VEC ? C / 4 : C;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int cv = int(idx % CV);
+        long long t = idx / CV;
+        const int wo = int(t % Wo); t /= Wo;
+        const int ho = int(t % Ho);
+        const long long b = t / Ho;
+        const long long base = ((b * H + 2 * ho) * W + 2 * wo);
+        if (VEC) {
+            f32x4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            int arg[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const long long pix = base + (q >> 1) * W + (q & 1);
+                f32x4 v = *reinterpret_cast<const f32x4*>(x + pix * C + cv * 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { float bb = best[e]; pool_take(v[e], q, bb, arg[e]); best[e] = bb; }
+            }
+            *reinterpret_cast<f32x4*>(y + idx * 4) = best;
+        } else {
+            float best = -INFINITY;
+            int arg = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const long long pix = base + (q >> 1) * W + (q & 1);
+                pool_take(x[pix * C + cv], q, best, arg);
+            }
+            y[idx] = best;
+        }
+    }
+}
+
+// One thread per INPUT element group (pixel, 4 channels): recompute the window's argmax and
+// route the pooled gradient to it; every other input element gets 0 (or keeps its value).
+template <bool VEC>
+__global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dx,
+                                   int H, int W, int C, int Ho, int Wo, int relu_mask, int accumulate,
+                                   long long total) {
+    constexpr int V = VEC ? 4 : 1;
+    const int CV = C / V;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int cv = int(idx % CV);
+        long long t = idx / CV;
+        const int wi = int(t % W); t /= W;
+        const int hi = int(t % H);
+        const long long b = t / H;
+        const int ho = hi >> 1, wo = wi >> 1;
+        float out[V];
+        float old[V];
+        if (accumulate) {
+#pragma unroll
+            for (int e = 0; e < V; ++e) old[e] = dx[idx * V + e];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) out[e] = 0.f;
+        if (ho < Ho && wo < Wo) {
+            const int me = (hi & 1) * 2 + (wi & 1);
+            const long long base = ((b * H + 2 * ho) * W + 2 * wo);
+            float best[V];
+            int arg[V];
+            float xme[V];
+#pragma unroll
+            for (int e = 0; e < V; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const long long pix = base + (q >> 1) * W + (q & 1);
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    float v = x[pix * C + cv * V + e];
+                    if (q == me) xme[e] = v;
+                    pool_take(v, q, best[e], arg[e]);
+                }
+            }
+            const long long oidx = ((b * Ho + ho) * Wo + wo) * C + cv * V;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                if (arg[e] == me && (!relu_mask || xme[e] > 0.f)) out[e] = dy[oidx + e];
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) dx[idx * V + e] = accumulate ? old[e] + out[e] : out[e];
+    }
+}
+
+// outconv forward: 16 lanes per pixel, each a float4 of channels; shuffle-reduce over the 16.
+__global__ void outconv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                                   float* __restrict__ y, long long rows, int C) {
+    const int lane16 = threadIdx.x & 15;
+    const long long groups = (long long)gridDim.x * (blockDim.x >> 4);
+    const float bias = b ? b[0] : 0.f;
+    for (long long m = blockIdx.x * (long long)(blockDim.x >> 4) + (threadIdx.x >> 4); m < rows + 0; m += groups) {
+        float s = 0.f;
+        for (int c = lane16 * 4; c < C; c += 64) {
+            f32x4 v = *reinterpret_cast<const f32x4*>(x + m * C + c);
+            f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+            s += v[0] * ww[0] + v[1] * ww[1] + v[2] * ww[2] + v[3] * ww[3];
+        }
+        s += __shfl_xor(s, 8, 16);
+        s += __shfl_xor(s, 4, 16);
+        s += __shfl_xor(s, 2, 16);
+        s += __shfl_xor(s, 1, 16);
+        if (lane16 == 0) y[m] = s + bias;
+    }
+}
+
+__global__ void outconv_fwd_scalar_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                          const float* __restrict__ b, float* __restrict__ y, long long rows, int C) {
+    for (long long m = blockIdx.x * (long long)blockDim.x + threadIdx.x; m < rows; m += (long long)gridDim.x * blockDim.x) {
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s += x[m * C + c] * w[c];
+        y[m] = s + (b ? b[0] : 0.f);
+    }
+}
+
+// outconv backward: dx = dy (x) w (masked); per-block partial sums of dw (C) and db.
+// Thread layout: 16 pixel groups x 16 lanes; lane owns channels lane*4 + 64*j.
+constexpr int OC_BLOCKS = 1024;
+
+__global__ void outconv_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ dy,
+                                   float* __restrict__ dx, float* __restrict__ partial, long long rows, int C,
+                                   int relu_mask) {
+    __shared__ float red[16][65];
+    __shared__ float redb[16];
+    const int lane16 = threadIdx.x & 15;
+    const int grp = threadIdx.x >> 4;
+    float* out = partial + (long long)blockIdx.x * (C + 1);
+    for (int j = 0; j * 64 < C; ++j) {
+        const int c = lane16 * 4 + 64 * j;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, ab = 0.f;
+        for (long long m = blockIdx.x * 16LL + grp; m < rows; m += (long long)gridDim.x * 16) {
+            const float g = dy[m];
+            ab += g;
+            if (c < C) {
+                f32x4 v = *reinterpret_cast<const f32x4*>(x + m * C + c);
+                f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+                f32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (!relu_mask || v[e] > 0.f) ? g * ww[e] : 0.f;
+                *reinterpret_cast<f32x4*>(dx + m * C + c) = o;
+                a0 += g * v[0]; a1 += g * v[1]; a2 += g * v[2]; a3 += g * v[3];
+            }
+        }
+        __syncthreads();
+        red[grp][lane16 * 4 + 0] = a0;
+        red[grp][lane16 * 4 + 1] = a1;
+        red[grp][lane16 * 4 + 2] = a2;
+        red[grp][lane16 * 4 + 3] = a3;
+        if (lane16 == 0) redb[grp] = ab;
+        __syncthreads();
+        const int t = threadIdx.x;
+        if (t < 64 && 64 * j + t < C) {
+            float s = 0.f;
+            for (int q = 0; q < 16; ++q) s += red[q][t];
+            out[64 * j + t] = s;
+        }
+        if (j == 0 && t == 64) {
+            float s = 0.f;
+            for (int q = 0; q < 16; ++q) s += redb[q];
+            out[C] = s;
+        }
+    }
+}
+
+__global__ void column_sum_kernel(const float* __restrict__ partial, int nparts, int cols, float* __restrict__ dw,
+                                  float* __restrict__ db) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > cols) return;
+    float s = 0.f;
+    for (int q = 0; q < nparts; ++q) s += partial[(long long)q * (cols + 1) + c];
+    if (c < cols) dw[c] = s;
+    else db[0] = s;
+}
+
+static int grid_for(long long total, int block = 256, int cap = 8192) {
+    long long g = (total + block - 1) / block;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace pu
+
+using namespace pu;
+
+extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw, int k_pad,
+                              void* stream) {
+    PU_REQUIRE(w && packed && d0 > 0 && d1 > 0 && kh > 0 && kw > 0 && k_pad > 0, "pu_pack_weight: bad args");
+    PU_REQUIRE(mode >= 0 && mode <= 3, "pu_pack_weight: mode %d", mode);
+    const int taps = kh * kw;
+    int rows, kmin;
+    switch (mode) {
+        case PU_PACK_CONV_FWD: rows = d0; kmin = taps * d1; break;
+        case PU_PACK_CONV_DGRAD: rows = d1; kmin = taps * d0; break;
+        case PU_PACK_CONVT_FWD: rows = taps * d1; kmin = d0; break;
+        default: rows = d0; kmin = taps * d1; break;
+    }
+    PU_REQUIRE(k_pad >= kmin, "pu_pack_weight: k_pad %d < %d", k_pad, kmin);
+    const long long total = (long long)rows * k_pad;
+    hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), w, packed, mode, d0,
+                       d1, kh, kw, k_pad, rows);
+    return check_launch("pu_pack_weight");
+}
+
+extern "C" int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, void* stream) {
+    PU_REQUIRE(src && dst && batch > 0 && c > 0 && h > 0 && w > 0, "pu_nchw_to_nhwc: bad args");
+    const long long total = (long long)batch * c * h * w;
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), src, dst, c, h * w,
+                       total);
+    return check_launch("pu_nchw_to_nhwc");
+}
+
+extern "C" int pu_maxpool2_fwd(const float* x, float* y, int batch, int h, int w, int c, void* stream) {
+    PU_REQUIRE(x && y && batch > 0 && h >= 2 && w >= 2 && c > 0, "pu_maxpool2_fwd: bad args");
+    const int ho = h / 2, wo = w / 2;
+    const bool vec = (c % 4 == 0) && (((uintptr_t)x | (uintptr_t)y) & 15) == 0;
+    const long long total = (long long)batch * ho * wo * (vec ? c / 4 : c);
+    if (vec)
+        hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, y, h, w,
+                           c, ho, wo, total);
+    else
+        hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, y, h,
+                           w, c, ho, wo, total);
+    return check_launch("pu_maxpool2_fwd");
+}
+
+extern "C" int pu_maxpool2_bwd(const float* x, const float* dy, float* dx, int batch, int h, int w, int c,
+                               int relu_mask, int accumulate, void* stream) {
+    PU_REQUIRE(x && dy && dx && batch > 0 && h >= 2 && w >= 2 && c > 0, "pu_maxpool2_bwd: bad args");
+    const int ho = h / 2, wo = w / 2;
+    const bool vec = (c % 4 == 0);
+    const long long total = (long long)batch * h * w * (vec ? c / 4 : c);
+    if (vec)
+        hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, dy, dx,
+                           h, w, c, ho, wo, relu_mask, accumulate, total);
+    else
+        hipLaunchKernelGGL(maxpool_bwd_kernel<false>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, dy, dx,
+                           h, w, c, ho, wo, relu_mask, accumulate, total);
+    return check_launch("pu_maxpool2_bwd");
+}
+
+extern "C" int pu_outconv_fwd(const float* x, const float* w, const float* b, float* y, long long rows, int c,
+                              void* stream) {
+    PU_REQUIRE(x && w && y && rows > 0 && c > 0, "pu_outconv_fwd: bad args");
+    if (c % 4 == 0 && (((uintptr_t)x | (uintptr_t)w) & 15) == 0) {
+        const long long groups = (rows + 15) / 16;
+        hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for(groups, 1, 8192)), dim3(256), 0, as_stream(stream), x, w,
+                           b, y, rows, c);
+    } else {
+        hipLaunchKernelGGL(outconv_fwd_scalar_kernel, dim3(grid_for(rows)), dim3(256), 0, as_stream(stream), x, w, b, y,
+                           rows, c);
+    }
+    return check_launch("pu_outconv_fwd");
+}
+
+extern "C" size_t pu_outconv_workspace_bytes(long long rows, int c) {
+    (void)rows;
+    return (size_t)OC_BLOCKS * (c + 1) * sizeof(float);
+}
+
+extern "C" int pu_outconv_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, float* db,
+                              long long rows, int c, int relu_mask, void* workspace, size_t ws_bytes, void* stream) {
+    PU_REQUIRE(x && w && dy && dx && dw && db && rows > 0, "pu_outconv_bwd: bad args");
+    PU_REQUIRE(c % 4 == 0, "pu_outconv_bwd: channels %d must be a multiple of 4", c);
+    PU_REQUIRE(((((uintptr_t)x | (uintptr_t)w | (uintptr_t)dx)) & 15) == 0, "pu_outconv_bwd: 16-byte alignment");
+    const size_t need = pu_outconv_workspace_bytes(rows, c);
+    if (!workspace || ws_bytes < need) return fail(PU_ERR_WORKSPACE, "pu_outconv_bwd: workspace %zu < %zu", ws_bytes, need);
+    int blocks = (int)((rows + 15) / 16);
+    if (blocks > OC_BLOCKS) blocks = OC_BLOCKS;
+    float* part = (float*)workspace;
+    hipLaunchKernelGGL(outconv_bwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, w, dy, dx, part, rows, c,
+                       relu_mask);
+    hipLaunchKernelGGL(column_sum_kernel, dim3((c + 1 + 255) / 256), dim3(256), 0, as_stream(stream), part, blocks, c,
+                       dw, db);
+    return check_launch("pu_outconv_bwd");
+}

@@ -1,0 +1,346 @@
+// Weight (and bias) gradients of the convolutions as split-K fp32 MFMA GEMMs.
+//
+// Replaces the autograd weight/bias backward of nn.Conv2d (src/unet/unet_p.py:184-201) and
+// nn.ConvTranspose2d (unet_p.py:238) that loss.backward() (src/train.py:110) runs on the CPU.
+//
+//   out[n][k] = sum_m P[m][n] * Q[m][k]      m = pixel rows (B*H*W), split over grid.z
+//   P = rows operand (conv: dZ; ConvT: its low-res input), Q = im2col of src0|src1 at tap(k)
+//   bias_mode 1 adds a ones COLUMN (k == K)  -> dbias[n]  = sum_m P[m][n]
+//   bias_mode 2 adds a ones ROW    (n == N)  -> dbias[c] = sum_taps sum_m Q[m][(tap,c)]
+// MFMA mapping (32x32x2): lane (i, h) supplies A[i][h] = P[m0+h][n_i] and B[h][j] = Q[m0+h][k_j],
+// both read from LDS with ds_read_b32 (32 consecutive floats per half-wave: conflict-free).
+// Partial tiles go to a per-split slab; wgrad_reduce sums the splits in a fixed order
+// (deterministic) and writes PyTorch's [n][c][kh][kw] layout.
+#include "common.h"
+
+namespace pu {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int WG_BM = 16;  // pixel rows per LDS stage
+
+struct WgradParams {
+    int M, N, Nr, K, Kc, C, c0, c1;
+    int Hi, Wi, Ho, Wo, kw, stride, pad;
+    const float* P;
+    const float* src0;
+    const float* src1;
+    int bias_mode;
+    float* slab;
+    int mps;  // pixel rows per split (multiple of WG_BM)
+    FastDiv dWo, dHo, dC, dKw;
+};
+
+template <int BN, int BK, int WN, int WK, bool QVEC>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
+    constexpr int FN = BN / WN / 32;
+    constexpr int FK = BK / WK / 32;
+    constexpr int P_PER_ROW = BN / 4;               // float4 per P row
+    constexpr int P_LD = (WG_BM * P_PER_ROW) / 256;  // float4 loads per thread
+    constexpr int Q_PER_ROW = BK / 4;
+    constexpr int Q_LD = (WG_BM * Q_PER_ROW) / 256;
+    static_assert(WN * WK == 4, "4 waves");
+    static_assert(P_LD >= 1 && Q_LD >= 1, "tile too small for 256 threads");
+
+    __shared__ __attribute__((aligned(16))) float lds[2 * WG_BM * (BN + BK)];
+    float* Ps = lds;
+    float* Qs = lds + 2 * WG_BM * BN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wn = wave % WN, wk = wave / WN;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int n_blk = blockIdx.y * BN;
+    const int k_blk = blockIdx.x * BK;
+    const int m_begin = blockIdx.z * p.mps;
+    const int m_end = min(p.M, m_begin + p.mps);
+
+    // ---- fixed per-thread P columns
+    const int p_col = (tid % P_PER_ROW) * 4;
+    const int p_row = tid / P_PER_ROW;               // + i * (256 / P_PER_ROW)
+    const int pn = n_blk + p_col;
+    // ---- fixed per-thread Q columns: tap offsets and channel
+    const int q_col = (tid % Q_PER_ROW) * 4;
+    const int q_row = tid / Q_PER_ROW;               // + i * (256 / Q_PER_ROW)
+    int q_r[4], q_s[4], q_c[4];
+    bool q_ok[4], q_one[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        // QVEC: the four columns share one tap (C % 4 == 0), so only element 0 is decoded
+        const int k = k_blk + q_col + e;
+        q_ok[e] = k < p.K;
+        q_one[e] = (p.bias_mode == 1) && k == p.K;
+        const int kk = q_ok[e] ? k : 0;
+        const int tap = fdiv(kk, p.dC);
+        q_c[e] = kk - tap * p.C;
+        q_r[e] = fdiv(tap, p.dKw);
+        q_s[e] = tap - q_r[e] * p.kw;
+        if (QVEC) break;
+    }
+
+    f32x4 rp[P_LD], rq[Q_LD];
+    auto load_stage = [&](int m0) {
+#pragma unroll
+        for (int i = 0; i < P_LD; ++i) {
+            int m = m0 + p_row + i * (256 / P_PER_ROW);
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (m < m_end) {
+                if (pn + 3 < p.N) {
+                    v = *reinterpret_cast<const f32x4*>(p.P + (long long)m * p.N + pn);
+                } else if (p.bias_mode == 2 && pn == p.N) {
+                    v[0] = 1.f;
+                }
+            }
+            rp[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < Q_LD; ++i) {
+            int m = m0 + q_row + i * (256 / Q_PER_ROW);
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (m < m_end) {
+                int t = fdiv(m, p.dWo);
+                int wo = m - t * p.Wo;
+                int b = fdiv(t, p.dHo);
+                int ho = t - b * p.Ho;
+                long long pb = (long long)b * p.Hi * p.Wi;
+                int hb = ho * p.stride - p.pad, wb = wo * p.stride - p.pad;
+                if (QVEC) {
+                    if (q_ok[0]) {
+                        int hi = hb + q_r[0], wi = wb + q_s[0];
+                        if ((unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi) {
+                            long long pix = pb + hi * p.Wi + wi;
+                            int c = q_c[0];
+                            const float* src = c < p.c0 ? p.src0 + pix * p.c0 + c : p.src1 + pix * p.c1 + (c - p.c0);
+                            v = *reinterpret_cast<const f32x4*>(src);
+                        }
+                    } else if (q_one[0]) {
+                        v[0] = 1.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (q_ok[e]) {
+                            int hi = hb + q_r[e], wi = wb + q_s[e];
+                            if ((unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi) {
+                                long long pix = pb + hi * p.Wi + wi;
+                                int c = q_c[e];
+                                v[e] = c < p.c0 ? p.src0[pix * p.c0 + c] : p.src1[pix * p.c1 + (c - p.c0)];
+                            }
+                        } else if (q_one[e]) {
+                            v[e] = 1.f;
+                        }
+                    }
+                }
+            }
+            rq[i] = v;
+        }
+    };
+    auto store_stage = [&](int buf) {
+        float* ps = Ps + buf * WG_BM * BN;
+        float* qs = Qs + buf * WG_BM * BK;
+#pragma unroll
+        for (int i = 0; i < P_LD; ++i)
+            *reinterpret_cast<f32x4*>(ps + (p_row + i * (256 / P_PER_ROW)) * BN + p_col) = rp[i];
+#pragma unroll
+        for (int i = 0; i < Q_LD; ++i)
+            *reinterpret_cast<f32x4*>(qs + (q_row + i * (256 / Q_PER_ROW)) * BK + q_col) = rq[i];
+    };
+
+    f32x16 acc[FN][FK];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FK; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int a_col0 = wn * (BN / WN) + lr;
+    const int b_col0 = wk * (BK / WK) + lr;
+
+    if (m_begin < m_end) {
+        load_stage(m_begin);
+        store_stage(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int m0 = m_begin; m0 < m_end; m0 += WG_BM) {
+        const bool more = m0 + WG_BM < m_end;
+        if (more) load_stage(m0 + WG_BM);
+        const float* ps = Ps + buf * WG_BM * BN;
+        const float* qs = Qs + buf * WG_BM * BK;
+#pragma unroll
+        for (int ks = 0; ks < WG_BM / 2; ++ks) {
+            float fa[FN], fb[FK];
+            const int row = ks * 2 + lh;
+#pragma unroll
+            for (int i = 0; i < FN; ++i) fa[i] = ps[row * BN + a_col0 + i * 32];
+#pragma unroll
+            for (int j = 0; j < FK; ++j) fb[j] = qs[row * BK + b_col0 + j * 32];
+#pragma unroll
+            for (int i = 0; i < FN; ++i)
+#pragma unroll
+                for (int j = 0; j < FK; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) store_stage(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+
+    // ---- partial tile -> slab[z][n][k]
+    float* slab = p.slab + (long long)blockIdx.z * p.Nr * p.Kc;
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+#pragma unroll
+        for (int j = 0; j < FK; ++j) {
+            const int k = k_blk + b_col0 + j * 32;
+            if (k >= p.Kc) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int n = n_blk + wn * (BN / WN) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (n < p.Nr) slab[(long long)n * p.Kc + k] = acc[i][j][r];
+            }
+        }
+    }
+}
+
+// Sum the per-split partials (fixed order) and scatter to [n][c][kh][kw] + bias.
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Nr, int Kc, int N, int K,
+                                    int C, int kh, int kw, int bias_mode, float* __restrict__ dw,
+                                    float* __restrict__ db, int accumulate) {
+    const long long total = (long long)Nr * Kc;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int n = int(idx / Kc);
+        const int k = int(idx - (long long)n * Kc);
+        float s = 0.f;
+        for (int z = 0; z < splits; ++z) s += slab[(long long)z * total + idx];
+        if (n < N && k < K) {
+            const int tap = k / C, c = k - tap * C;
+            const int r = tap / kw, ss = tap - r * kw;
+            float* o = dw + (((long long)n * C + c) * kh + r) * kw + ss;
+            *o = accumulate ? *o + s : s;
+        } else if (bias_mode == 1 && n < N && k == K) {
+            db[n] = accumulate ? db[n] + s : s;
+        }
+    }
+}
+
+// ConvT bias (bias_mode 2): db[c] = sum over taps of the ones-row partial sums
+__global__ void wgrad_bias_rows_kernel(const float* __restrict__ slab, int splits, int Nr, int Kc, int N, int C,
+                                       int taps, float* __restrict__ db, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const long long total = (long long)Nr * Kc;
+    float s = 0.f;
+    for (int t = 0; t < taps; ++t) {
+        float st = 0.f;
+        for (int z = 0; z < splits; ++z) st += slab[(long long)z * total + (long long)N * Kc + t * C + c];
+        s += st;
+    }
+    db[c] = accumulate ? db[c] + s : s;
+}
+
+struct WgradPlan {
+    int BN, BK, splits, mps, Nr, Kc, M, K, C;
+    bool qvec;
+};
+
+static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
+    PU_REQUIRE(a && a->batch > 0 && a->out_h > 0 && a->out_w > 0 && a->in_h > 0 && a->in_w > 0, "pu_wgrad: bad grid");
+    PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0, "pu_wgrad: bad taps");
+    PU_REQUIRE(a->rows && a->n > 0 && a->src0 && a->c0 > 0 && (a->c1 == 0 || a->src1), "pu_wgrad: operands");
+    PU_REQUIRE(a->n % 4 == 0, "pu_wgrad: n (%d) must be a multiple of 4", a->n);
+    PU_REQUIRE(a->bias_mode >= 0 && a->bias_mode <= 2, "pu_wgrad: bias_mode");
+    PU_REQUIRE(a->bias_mode == 0 || a->dbias, "pu_wgrad: dbias missing");
+    PU_REQUIRE(a->dweight, "pu_wgrad: dweight missing");
+    const long long M = (long long)a->batch * a->out_h * a->out_w;
+    PU_REQUIRE(M < (1LL << 31), "pu_wgrad: too many pixels");
+    pl->M = (int)M;
+    pl->C = a->c0 + a->c1;
+    pl->K = a->kh * a->kw * pl->C;
+    pl->Nr = a->n + (a->bias_mode == 2 ? 1 : 0);
+    pl->Kc = pl->K + (a->bias_mode == 1 ? 1 : 0);
+    pl->qvec = (a->c0 % 4 == 0) && (a->c1 % 4 == 0);
+    if (pl->qvec) {
+        PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0, "pu_wgrad: sources must be 16-byte aligned");
+    }
+    PU_REQUIRE(((uintptr_t)a->rows & 15) == 0, "pu_wgrad: rows must be 16-byte aligned");
+    if (pl->Kc <= 64) { pl->BN = 64; pl->BK = 64; }
+    else if (pl->Nr <= 64) { pl->BN = 64; pl->BK = 256; }
+    else { pl->BN = 128; pl->BK = 128; }
+    const int tiles = ceil_div(pl->Nr, pl->BN) * ceil_div(pl->Kc, pl->BK);
+    int splits = ceil_div(768, tiles);
+    int max_splits = ceil_div(M, 256);
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    int mps = ceil_div(ceil_div(M, splits), WG_BM) * WG_BM;
+    pl->mps = mps;
+    pl->splits = ceil_div(M, mps);
+    return PU_OK;
+}
+
+}  // namespace pu
+
+using namespace pu;
+
+extern "C" size_t pu_wgrad_workspace_bytes(const pu_wgrad_args* a) {
+    WgradPlan pl;
+    if (plan_wgrad(a, &pl) != PU_OK) return 0;
+    return (size_t)pl.splits * pl.Nr * pl.Kc * sizeof(float);
+}
+
+extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec, int* splits) {
+    WgradPlan pl;
+    int st = plan_wgrad(a, &pl);
+    if (st != PU_OK) return st;
+    if (bn) *bn = pl.BN;
+    if (bk) *bk = pl.BK;
+    if (qvec) *qvec = pl.qvec ? 1 : 0;
+    if (splits) *splits = pl.splits;
+    return PU_OK;
+}
+
+extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes, void* stream) {
+    WgradPlan pl;
+    int st = plan_wgrad(a, &pl);
+    if (st != PU_OK) return st;
+    const size_t need = (size_t)pl.splits * pl.Nr * pl.Kc * sizeof(float);
+    if (!workspace || ws_bytes < need)
+        return fail(PU_ERR_WORKSPACE, "pu_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+
+    WgradParams p;
+    p.M = pl.M; p.N = a->n; p.Nr = pl.Nr; p.K = pl.K; p.Kc = pl.Kc; p.C = pl.C; p.c0 = a->c0; p.c1 = a->c1;
+    p.Hi = a->in_h; p.Wi = a->in_w; p.Ho = a->out_h; p.Wo = a->out_w;
+    p.kw = a->kw; p.stride = a->stride; p.pad = a->pad;
+    p.P = a->rows; p.src0 = a->src0; p.src1 = a->src1; p.bias_mode = a->bias_mode;
+    p.slab = (float*)workspace; p.mps = pl.mps;
+    p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
+    p.dC = make_fastdiv(pl.C); p.dKw = make_fastdiv(a->kw);
+
+    hipStream_t s = as_stream(stream);
+    dim3 grid(ceil_div(pl.Kc, pl.BK), ceil_div(pl.Nr, pl.BN), pl.splits);
+#define PU_WG_LAUNCH(BN_, BK_, WN_, WK_)                                                              \
+    do {                                                                                               \
+        if (pl.qvec) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, true>), grid, dim3(256), 0, s, p);  \
+        else hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, false>), grid, dim3(256), 0, s, p);         \
+    } while (0)
+    if (pl.BK == 64) PU_WG_LAUNCH(64, 64, 2, 2);
+    else if (pl.BK == 256) PU_WG_LAUNCH(64, 256, 1, 4);
+    else PU_WG_LAUNCH(128, 128, 2, 2);
+#undef PU_WG_LAUNCH
+    st = check_launch("pu_wgrad (gemm)");
+    if (st != PU_OK) return st;
+
+    const long long total = (long long)pl.Nr * pl.Kc;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)workspace, pl.splits, pl.Nr,
+                       pl.Kc, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias, a->accumulate);
+    if (a->bias_mode == 2) {
+        hipLaunchKernelGGL(wgrad_bias_rows_kernel, dim3(ceil_div(pl.C, 256)), dim3(256), 0, s, (const float*)workspace,
+                           pl.splits, pl.Nr, pl.Kc, a->n, pl.C, a->kh * a->kw, a->dbias, a->accumulate);
+    }
+    return check_launch("pu_wgrad (reduce)");
+}

@@ -1,0 +1,114 @@
+"""ctypes binding of libplastic_unet.so (include/plastic_unet.h).
+
+The library is the product's only compute path: importing a kernel wrapper without it raises
+immediately - there is no CPU or eager-PyTorch fallback.  torch is imported first so the HIP
+runtime torch ships (libamdhip64.so.7) is the one the library binds to; our kernels then run on
+torch's streams and device memory.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must load the HIP runtime before the library)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PLASTIC_UNET_LIB",
+                          os.path.join(os.path.dirname(HERE), "lib", "libplastic_unet.so"))
+
+c_int, c_ll, c_size, c_float, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
+P = ctypes.c_void_p
+
+PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2 = 1, 2, 4
+PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD = 0, 1, 2, 3
+PU_RULE_HEBB, PU_RULE_OJA = 0, 1
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [("batch", c_int), ("in_h", c_int), ("in_w", c_int), ("out_h", c_int), ("out_w", c_int),
+                ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int),
+                ("src0", P), ("c0", c_int), ("src1", P), ("c1", c_int),
+                ("weight", P), ("k_pad", c_int), ("n", c_int), ("bias", P),
+                ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int)]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [("batch", c_int), ("in_h", c_int), ("in_w", c_int), ("out_h", c_int), ("out_w", c_int),
+                ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int),
+                ("rows", P), ("n", c_int), ("src0", P), ("c0", c_int), ("src1", P), ("c1", c_int),
+                ("bias_mode", c_int), ("dweight", P), ("dbias", P), ("accumulate", c_int)]
+
+
+class PlasticArgs(ctypes.Structure):
+    _fields_ = [("batch", c_int), ("nbf", c_int), ("x", P), ("hebb", P), ("w", P), ("alpha", P), ("eta", P),
+                ("y", P), ("hebb_out", P), ("rule", c_int)]
+
+
+class PlasticBwdArgs(ctypes.Structure):
+    _fields_ = [("batch", c_int), ("nbf", c_int), ("x", P), ("hebb", P), ("w", P), ("alpha", P), ("y", P),
+                ("dy", P), ("dx", P), ("dw", P), ("dalpha", P)]
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", P), ("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("numel", c_ll)]
+
+
+# every symbol declared in include/plastic_unet.h: (name, restype, argtypes)
+SIGNATURES = [
+    ("pu_abi_version", c_int, []),
+    ("pu_last_error", ctypes.c_char_p, []),
+    ("pu_device_info", c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_ll)]),
+    ("pu_conv_igemm", c_int, [ctypes.POINTER(ConvArgs), P]),
+    ("pu_conv_igemm_tile", c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                   ctypes.POINTER(c_int)]),
+    ("pu_wgrad_workspace_bytes", c_size, [ctypes.POINTER(WgradArgs)]),
+    ("pu_wgrad", c_int, [ctypes.POINTER(WgradArgs), P, c_size, P]),
+    ("pu_wgrad_tile", c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                              ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    ("pu_nchw_to_nhwc", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    ("pu_maxpool2_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    ("pu_maxpool2_bwd", c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    ("pu_outconv_fwd", c_int, [P, P, P, P, c_ll, c_int, P]),
+    ("pu_outconv_workspace_bytes", c_size, [c_ll, c_int]),
+    ("pu_outconv_bwd", c_int, [P, P, P, P, P, P, c_ll, c_int, c_int, P, c_size, P]),
+    ("pu_plastic_fwd", c_int, [ctypes.POINTER(PlasticArgs), P]),
+    ("pu_trace_update", c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
+    ("pu_plastic_bwd_workspace_bytes", c_size, [c_int, c_int]),
+    ("pu_plastic_bwd", c_int, [ctypes.POINTER(PlasticBwdArgs), P, c_size, P]),
+    ("pu_bce_workspace_bytes", c_size, [c_ll]),
+    ("pu_bce_fwd", c_int, [P, P, c_ll, P, P, c_size, P]),
+    ("pu_bce_bwd", c_int, [P, P, c_ll, P, P, P]),
+    ("pu_adam_multi", c_int, [ctypes.POINTER(AdamTensor), c_int, c_float, c_float, c_float, c_float, c_float,
+                              c_float, P]),
+]
+
+_lib = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and type the library; raise LibraryMissing if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LibraryMissing(
+            "libplastic_unet.so not found at %s - build it with `python plastic-unet_amd/build_native.py` "
+            "(the plastic U-Net path has no CPU fallback)" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.pu_abi_version() != 1:
+        raise LibraryMissing("libplastic_unet.so ABI %d != 1" % lib.pu_abi_version())
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = _lib.pu_last_error().decode(errors="replace") if _lib is not None else ""
+        raise RuntimeError("%s failed (%d): %s" % (what or "plastic_unet call", rc, msg))

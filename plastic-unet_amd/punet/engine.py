@@ -1,0 +1,46 @@
+"""Batched training step of the plastic U-Net (the hot loop of src/train.py:91-112, batched).
+
+    trainer = Trainer(net, lr=3e-4, steplr=1e5)     # FusedAdam + StepLR(gamma .666), per step
+    loss, hebb = trainer.step(x, t, hebb)           # fwd -> BCE -> bwd -> [RCCL all-reduce] -> Adam
+
+Batched semantics: slot b of step s carries its trace to slot b of step
+s+1; loss = mean BCE over all slots' pixels (so each slot contributes the reference's per-sample
+gradient / B).  Under data parallelism each rank runs its own slots (the global batch is sharded
+contiguously by rank) and gradients are averaged across ranks; traces stay per rank.
+"""
+import torch
+import torch.distributed as dist
+
+from . import dp
+from .head import bce_loss
+from .optim import FusedAdam
+
+
+class Trainer:
+    def __init__(self, net, lr=3e-4, steplr=1e5, gamma=0.666, betas=(0.9, 0.999), eps=1e-8,
+                 flat_grads=True, bucket_mb=32):
+        self.net = net
+        self.params = list(net.parameters())
+        self.opt = FusedAdam(net.parameters(), lr=lr, betas=betas, eps=eps)
+        self.sched = torch.optim.lr_scheduler.StepLR(self.opt, gamma=gamma, step_size=int(steplr))
+        self.bucket_mb = bucket_mb
+        self.gradbuf = None
+        if flat_grads and hasattr(net, "_trunk_plan"):
+            trainable = [p for p in self.params if p is not net.eta]
+            self.gradbuf = dp.GradBuffer(trainable, next(net.parameters()).device)
+            net._trunk_plan().gradbuf = self.gradbuf
+        self.distributed = dist.is_initialized() and dist.get_world_size() > 1
+
+    def step(self, x, t, hebb):
+        """One optimisation step on the local batch.  Returns (loss tensor, new hebb), both
+        detached and still on the device (no host synchronisation)."""
+        for p in self.params:
+            p.grad = None
+        y, hn = self.net(x, hebb.detach())
+        loss = bce_loss(y, t)
+        loss.backward()
+        if self.distributed:
+            dp.allreduce_grads(self.params, self.gradbuf, bucket_mb=self.bucket_mb)
+        self.opt.step()
+        self.sched.step()
+        return loss.detach(), hn.detach()

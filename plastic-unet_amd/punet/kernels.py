@@ -1,0 +1,301 @@
+"""torch-tensor wrappers over the C-ABI kernels (one wrapper per entry point of plastic_unet.h).
+
+Every wrapper enqueues on torch's *current* HIP stream and never synchronises.  Tensors must be
+fp32, contiguous and resident on the ROCm device; activations are NHWC.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticBwdArgs, AdamTensor, check,
+                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2)
+
+__all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
+           "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
+           "bce_bwd", "adam_multi", "round16", "device_info", "lib"]
+
+
+def lib():
+    return _lib.load()
+
+
+# ------------------------------------------------------------------------------ launch profiler
+_PROF = None
+_MODES = {0: "chunk16", 1: "vec4", 2: "scalar"}
+
+
+class KernelProfiler:
+    """Brackets every wrapped launch with HIP events on the stream it is launched on, tagged with
+    the kernel instantiation and its algorithmic FLOPs / bytes.  Use as a context manager."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _PROF
+        self._prev, _PROF = _PROF, self
+        return self
+
+    def __exit__(self, *exc):
+        global _PROF
+        _PROF = self._prev
+        return False
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for tag, flops, nbytes, e0, e1 in self.records:
+            d = out.setdefault(tag, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["flops"] += flops
+            d["bytes"] += nbytes
+        return out
+
+
+class _Rec:
+    __slots__ = ("tag", "flops", "nbytes", "e0")
+
+    def __init__(self, tag, flops=0.0, nbytes=0.0):
+        self.tag, self.flops, self.nbytes = tag, flops, nbytes
+        self.e0 = None
+
+    def __enter__(self):
+        if _PROF is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _PROF is not None and self.e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            _PROF.records.append((self.tag, self.flops, self.nbytes, self.e0, e1))
+        return False
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def round16(k):
+    return (k + 15) // 16 * 16
+
+
+def _req(t, name):
+    if t is None:
+        return
+    if not t.is_cuda:
+        raise RuntimeError("%s must be on the ROCm device (got %s); the plastic U-Net path has no CPU "
+                           "fallback" % (name, t.device))
+    if t.dtype != torch.float32:
+        raise RuntimeError("%s must be float32 (got %s)" % (name, t.dtype))
+    if not t.is_contiguous():
+        raise RuntimeError("%s must be contiguous" % name)
+
+
+def device_info(device=0):
+    L = lib()
+    cu, clk, mem = ctypes.c_int(), ctypes.c_int(), ctypes.c_longlong()
+    check(L.pu_device_info(device, ctypes.byref(cu), ctypes.byref(clk), ctypes.byref(mem)), "pu_device_info")
+    return cu.value, clk.value, mem.value
+
+
+def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, dst0, n0=None,
+          src1=None, c1=0, bias=None, dst1=None, mask0=None, mask1=None, relu=False, accum=False,
+          shuffle=False):
+    """pu_conv_igemm: implicit-GEMM conv (3x3 fwd/dgrad, ConvT fwd with shuffle, ConvT dgrad)."""
+    for t, nm in ((src0, "src0"), (src1, "src1"), (weight, "weight"), (bias, "bias"), (dst0, "dst0"),
+                  (dst1, "dst1"), (mask0, "mask0"), (mask1, "mask1")):
+        _req(t, nm)
+    flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0)
+    a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
+                 _p(src0), c0, _p(src1), c1, _p(weight), k_pad, n, _p(bias),
+                 _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags)
+    if _PROF is None:
+        check(lib().pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
+        return
+    bm, bn, mode = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    lib().pu_conv_igemm_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(mode))
+    M = batch * out_hw[0] * out_hw[1]
+    tag = "igemm<%dx%d,%s>" % (bm.value, bn.value, _MODES[mode.value])
+    with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
+        check(lib().pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
+
+
+def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, src1=None, c1=0,
+          bias_mode=0, dbias=None, accumulate=False):
+    """pu_wgrad: split-K weight (+bias) gradient into PyTorch's [n][c][k][k] layout."""
+    for t, nm in ((rows, "rows"), (src0, "src0"), (src1, "src1"), (dweight, "dweight"), (dbias, "dbias")):
+        _req(t, nm)
+    a = WgradArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
+                  _p(rows), n, _p(src0), c0, _p(src1), c1, bias_mode, _p(dweight), _p(dbias),
+                  1 if accumulate else 0)
+    L = lib()
+    nbytes = L.pu_wgrad_workspace_bytes(ctypes.byref(a))
+    if nbytes == 0:
+        check(L.pu_wgrad(ctypes.byref(a), None, 0, _stream()), "pu_wgrad")
+    ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=rows.device)
+    if _PROF is None:
+        check(L.pu_wgrad(ctypes.byref(a), ws.data_ptr(), nbytes, _stream()), "pu_wgrad")
+        return
+    bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
+    M = batch * out_hw[0] * out_hw[1]
+    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, "vec4" if qv.value else "scalar")
+    with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
+        check(L.pu_wgrad(ctypes.byref(a), ws.data_ptr(), nbytes, _stream()), "pu_wgrad")
+
+
+def pack_weight(w, mode, k_pad, out=None):
+    _req(w, "w")
+    d0, d1, kh, kw = w.shape
+    taps = kh * kw
+    rows = {0: d0, 1: d1, 2: taps * d1, 3: d0}[mode]
+    if out is None:
+        out = torch.empty(rows, k_pad, dtype=torch.float32, device=w.device)
+    with _Rec("pack_weight", nbytes=4.0 * (w.numel() + out.numel())):
+        check(lib().pu_pack_weight(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, _stream()),
+              "pu_pack_weight")
+    return out
+
+
+def nchw_to_nhwc(x):
+    _req(x, "x")
+    B, C, H, W = x.shape
+    out = torch.empty(B, H, W, C, dtype=torch.float32, device=x.device)
+    check(lib().pu_nchw_to_nhwc(x.data_ptr(), out.data_ptr(), B, C, H, W, _stream()), "pu_nchw_to_nhwc")
+    return out
+
+
+def maxpool2_fwd(x):
+    _req(x, "x")
+    B, H, W, C = x.shape
+    y = torch.empty(B, H // 2, W // 2, C, dtype=torch.float32, device=x.device)
+    with _Rec("maxpool_fwd", nbytes=4.0 * (x.numel() + y.numel())):
+        check(lib().pu_maxpool2_fwd(x.data_ptr(), y.data_ptr(), B, H, W, C, _stream()), "pu_maxpool2_fwd")
+    return y
+
+
+def maxpool2_bwd(x, dy, dx, relu_mask=True, accumulate=True):
+    _req(x, "x"); _req(dy, "dy"); _req(dx, "dx")
+    B, H, W, C = x.shape
+    with _Rec("maxpool_bwd", nbytes=4.0 * (x.numel() * (3 if accumulate else 2) + dy.numel())):
+        check(lib().pu_maxpool2_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C, int(relu_mask),
+                                    int(accumulate), _stream()), "pu_maxpool2_bwd")
+    return dx
+
+
+def outconv_fwd(x, w, b):
+    """x [B,H,W,C] NHWC, w [C] (flattened [1,C,1,1]), b [1] -> logits [B,H,W]."""
+    _req(x, "x"); _req(w, "w"); _req(b, "b")
+    B, H, W, C = x.shape
+    y = torch.empty(B, H, W, dtype=torch.float32, device=x.device)
+    with _Rec("outconv_fwd", nbytes=4.0 * (x.numel() + y.numel())):
+        check(lib().pu_outconv_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), B * H * W, C, _stream()),
+              "pu_outconv_fwd")
+    return y
+
+
+def outconv_bwd(x, w, dy, relu_mask=True, out=None):
+    _req(x, "x"); _req(w, "w"); _req(dy, "dy")
+    B, H, W, C = x.shape
+    rows = B * H * W
+    dx = torch.empty_like(x)
+    if out is None:
+        dw = torch.empty(C, dtype=torch.float32, device=x.device)
+        db = torch.empty(1, dtype=torch.float32, device=x.device)
+    else:
+        dw, db = out
+    L = lib()
+    nbytes = L.pu_outconv_workspace_bytes(rows, C)
+    ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=x.device)
+    with _Rec("outconv_bwd", nbytes=4.0 * (2 * x.numel() + rows)):
+        check(L.pu_outconv_bwd(x.data_ptr(), w.data_ptr(), dy.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                               rows, C, int(relu_mask), ws.data_ptr(), nbytes, _stream()), "pu_outconv_bwd")
+    return dx, dw, db
+
+
+def plastic_fwd(x, hebb, w, alpha, eta, rule, update_trace=True):
+    """x, hebb [B,N,N] -> (y [B,N,N], hebb' [B,N,N] or None)."""
+    for t, nm in ((x, "x"), (hebb, "hebb"), (w, "w"), (alpha, "alpha"), (eta, "eta")):
+        _req(t, nm)
+    B, N, _ = x.shape
+    y = torch.empty_like(x)
+    hn = torch.empty_like(hebb) if update_trace else None
+    a = PlasticArgs(B, N, x.data_ptr(), hebb.data_ptr(), w.data_ptr(), alpha.data_ptr(), eta.data_ptr(),
+                    y.data_ptr(), _p(hn), rule)
+    with _Rec("plastic_fwd", flops=2.0 * B * N ** 3, nbytes=4.0 * (4 * B * N * N + 2 * N * N)):
+        check(lib().pu_plastic_fwd(ctypes.byref(a), _stream()), "pu_plastic_fwd")
+    return y, hn
+
+
+def trace_update(hebb, x, y, eta, rule, out=None):
+    for t, nm in ((hebb, "hebb"), (x, "x"), (y, "y"), (eta, "eta")):
+        _req(t, nm)
+    B, N, _ = hebb.shape
+    out = torch.empty_like(hebb) if out is None else out
+    with _Rec("trace_update", nbytes=8.0 * B * N * N + 8.0 * B * N):
+        _trace(hebb, x, y, eta, out, B, N, rule)
+    return out
+
+
+def _trace(hebb, x, y, eta, out, B, N, rule):
+    check(lib().pu_trace_update(hebb.data_ptr(), x.data_ptr(), y.data_ptr(), eta.data_ptr(), out.data_ptr(), B, N,
+                                rule, _stream()), "pu_trace_update")
+
+
+def plastic_bwd(x, hebb, w, alpha, y, dy, need_dx=True, need_dw=True, out=None):
+    for t, nm in ((x, "x"), (hebb, "hebb"), (w, "w"), (alpha, "alpha"), (y, "y"), (dy, "dy")):
+        _req(t, nm)
+    B, N, _ = x.shape
+    dx = torch.empty_like(x) if need_dx else None
+    if out is not None and need_dw:
+        dw, da = out
+    else:
+        dw = torch.empty_like(w) if need_dw else None
+        da = torch.empty_like(alpha) if need_dw else None
+    L = lib()
+    nbytes = L.pu_plastic_bwd_workspace_bytes(B, N)
+    ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=x.device) if need_dw else None
+    a = PlasticBwdArgs(B, N, x.data_ptr(), hebb.data_ptr(), w.data_ptr(), alpha.data_ptr(), y.data_ptr(),
+                       dy.data_ptr(), _p(dx), _p(dw), _p(da))
+    with _Rec("plastic_bwd", flops=4.0 * B * N ** 3):
+        check(L.pu_plastic_bwd(ctypes.byref(a), _p(ws), nbytes if need_dw else 0, _stream()), "pu_plastic_bwd")
+    return dx, dw, da
+
+
+def bce_fwd(y, t):
+    _req(y, "y"); _req(t, "t")
+    n = y.numel()
+    if t.numel() != n:
+        raise ValueError("Target size (%s) must be the same as input size (%s)" % (tuple(t.shape), tuple(y.shape)))
+    L = lib()
+    nbytes = L.pu_bce_workspace_bytes(n)
+    ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=y.device)
+    loss = torch.empty((), dtype=torch.float32, device=y.device)
+    check(L.pu_bce_fwd(y.data_ptr(), t.data_ptr(), n, loss.data_ptr(), ws.data_ptr(), nbytes, _stream()), "pu_bce_fwd")
+    return loss
+
+
+def bce_bwd(y, t, grad_loss):
+    _req(y, "y"); _req(t, "t")
+    dy = torch.empty_like(y)
+    g = grad_loss.contiguous() if grad_loss is not None else None
+    check(lib().pu_bce_bwd(y.data_ptr(), t.data_ptr(), y.numel(), _p(g), dy.data_ptr(), _stream()), "pu_bce_bwd")
+    return dy
+
+
+def adam_multi(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt):
+    n = len(params)
+    arr = (AdamTensor * max(n, 1))()
+    for i, (p, g, m, v) in enumerate(zip(params, grads, exp_avgs, exp_avg_sqs)):
+        arr[i] = AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel())
+    with _Rec("adam", nbytes=28.0 * sum(p.numel() for p in params)):
+        check(lib().pu_adam_multi(arr, n, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, _stream()),
+              "pu_adam_multi")

@@ -1,0 +1,269 @@
+"""The U-Net trunk of UNetp as one autograd node whose forward and backward are sequences of
+HIP kernel launches (no ATen compute ops).
+
+Reference: yaricom/Plastic-UNet src/unet/unet_p.py:54-67 (forward) and the blocks at :179-260;
+the backward is what ``loss.backward()`` (src/train.py:110) runs through ATen on the CPU.
+
+Forward (NHWC, fp32), per stage:
+  inc     : conv3x3+ReLU, conv3x3+ReLU
+  down_i  : MaxPool2d(2) -> conv3x3+ReLU -> conv3x3+ReLU
+  up_j    : ConvT2x2s2 (GEMM + pixel-shuffle epilogue) -> conv3x3+ReLU over [skip | upsampled]
+            read from two buffers (no concat copy) -> conv3x3+ReLU
+  outc    : 1x1 conv C -> 1 (logits)
+Backward fuses every ReLU mask into the producing kernel's epilogue (dgrad / maxpool-bwd /
+outconv-bwd multiply by (activation > 0)), writes skip gradients once and lets the max-pool
+backward accumulate into them, and gets bias gradients from the weight-gradient GEMM (a ones
+column / ones row), so no separate elementwise or reduction passes run.
+"""
+import torch
+
+from . import kernels as K
+from ._lib import PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD
+
+
+class _Packs:
+    """Packed GEMM operands of the OIHW parameters, rebuilt only when a parameter changes."""
+
+    def __init__(self):
+        self.cache = {}
+
+    def get(self, w, mode, k_pad):
+        # keyed by storage (detached views share the parameter's version counter)
+        key = (w.data_ptr(), tuple(w.shape), mode)
+        ver = w._version
+        hit = self.cache.get(key)
+        if hit is not None and hit[0] == ver:
+            return hit[1]
+        packed = K.pack_weight(w.detach(), mode, k_pad)
+        self.cache[key] = (ver, packed)
+        return packed
+
+
+def conv3x3(x0, w, b, packs, x1=None, relu=True):
+    """3x3/p1 conv (+bias, ReLU) over the channel concat [x0 | x1] (NHWC)."""
+    B, H, W, c0 = x0.shape
+    c1 = 0 if x1 is None else x1.shape[3]
+    cout = w.shape[0]
+    k_pad = K.round16(9 * (c0 + c1))
+    out = torch.empty(B, H, W, cout, dtype=torch.float32, device=x0.device)
+    K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=x0, c0=c0, src1=x1, c1=c1,
+            weight=packs.get(w, PU_PACK_CONV_FWD, k_pad), k_pad=k_pad, n=cout, bias=b, dst0=out, relu=relu)
+    return out
+
+
+def conv3x3_dgrad(dz, w, packs, split=None, mask0=None, mask1=None):
+    """dX = conv(dZ, flipped W^T); optional channel split [0,split) -> d0, rest -> d1 and masks."""
+    B, H, W, cout = dz.shape
+    cin = w.shape[1]
+    k_pad = K.round16(9 * cout)
+    n0 = cin if split is None else split
+    d0 = torch.empty(B, H, W, n0, dtype=torch.float32, device=dz.device)
+    d1 = None if split is None else torch.empty(B, H, W, cin - n0, dtype=torch.float32, device=dz.device)
+    K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=dz, c0=cout,
+            weight=packs.get(w, PU_PACK_CONV_DGRAD, k_pad), k_pad=k_pad, n=cin, dst0=d0, n0=n0, dst1=d1,
+            mask0=mask0, mask1=mask1)
+    return d0, d1
+
+
+def conv3x3_wgrad(dz, x0, x1=None, out=None):
+    B, H, W, cout = dz.shape
+    c0 = x0.shape[3]
+    c1 = 0 if x1 is None else x1.shape[3]
+    if out is None:
+        dw = torch.empty(cout, c0 + c1, 3, 3, dtype=torch.float32, device=dz.device)
+        db = torch.empty(cout, dtype=torch.float32, device=dz.device)
+    else:
+        dw, db = out
+    K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, rows=dz, n=cout, src0=x0, c0=c0,
+            src1=x1, c1=c1, bias_mode=1, dweight=dw, dbias=db)
+    return dw, db
+
+
+def convT2x2(x, w, b, packs):
+    """ConvTranspose2d(cin, cout, 2, stride=2): GEMM [B*h*w, cin] x [cin, 4*cout] + pixel shuffle."""
+    B, h, wd, cin = x.shape
+    cout = w.shape[1]
+    k_pad = K.round16(cin)
+    out = torch.empty(B, 2 * h, 2 * wd, cout, dtype=torch.float32, device=x.device)
+    K.igemm(batch=B, in_hw=(h, wd), out_hw=(h, wd), k=1, stride=1, pad=0, src0=x, c0=cin,
+            weight=packs.get(w, PU_PACK_CONVT_FWD, k_pad), k_pad=k_pad, n=4 * cout, bias=b, dst0=out,
+            shuffle=True)
+    return out
+
+
+def convT2x2_dgrad(du, w, packs, mask):
+    """dX[b,h,w,:] = sum_(i,j) dU[b,2h+i,2w+j,:] W[:, :, i, j]^T, times (mask > 0)."""
+    B, H2, W2, cout = du.shape
+    cin = w.shape[0]
+    k_pad = K.round16(4 * cout)
+    dx = torch.empty(B, H2 // 2, W2 // 2, cin, dtype=torch.float32, device=du.device)
+    K.igemm(batch=B, in_hw=(H2, W2), out_hw=(H2 // 2, W2 // 2), k=2, stride=2, pad=0, src0=du, c0=cout,
+            weight=packs.get(w, PU_PACK_CONVT_DGRAD, k_pad), k_pad=k_pad, n=cin, dst0=dx, mask0=mask)
+    return dx
+
+
+def convT2x2_wgrad(x, du, out=None):
+    B, h, wd, cin = x.shape
+    cout = du.shape[3]
+    if out is None:
+        dw = torch.empty(cin, cout, 2, 2, dtype=torch.float32, device=x.device)
+        db = torch.empty(cout, dtype=torch.float32, device=x.device)
+    else:
+        dw, db = out
+    K.wgrad(batch=B, in_hw=(2 * h, 2 * wd), out_hw=(h, wd), k=2, stride=2, pad=0, rows=x, n=cin, src0=du,
+            c0=cout, bias_mode=2, dweight=dw, dbias=db)
+    return dw, db
+
+
+def as_nhwc_input(x):
+    """Model input [B,C,H,W] -> NHWC.  C == 1 is already NHWC in memory."""
+    x = x.contiguous()
+    if x.shape[1] == 1:
+        B, _, H, W = x.shape
+        return x.view(B, H, W, 1)
+    return K.nchw_to_nhwc(x)
+
+
+class UNetpTrunk:
+    """Parameter order and kernel schedule of the generalised UNetp trunk (depth D)."""
+
+    def __init__(self, model):
+        self.depth = model.depth
+        self.names = []
+        self.packs = _Packs()
+        mods = {"inc": model.inc.conv.conv}
+        for i in range(1, self.depth):
+            mods["down%d" % i] = getattr(model, "down%d" % i).mpconv[1].conv
+        for j in range(1, self.depth):
+            up = getattr(model, "up%d" % j)
+            mods["up%d.up" % j] = up.up
+            mods["up%d" % j] = up.conv.conv
+        self.params = []
+        # order: inc c0 w,b, c1 w,b ; down_i ... ; up_j: up w,b, c0 w,b, c1 w,b ; outc w,b
+        for key in ["inc"] + ["down%d" % i for i in range(1, self.depth)]:
+            seq = mods[key]
+            for idx in (0, 2):
+                self.params += [seq[idx].weight, seq[idx].bias]
+        for j in range(1, self.depth):
+            upm = mods["up%d.up" % j]
+            self.params += [upm.weight, upm.bias]
+            seq = mods["up%d" % j]
+            for idx in (0, 2):
+                self.params += [seq[idx].weight, seq[idx].bias]
+        self.params += [model.outc.conv.weight, model.outc.conv.bias]
+        self.gradbuf = None      # punet.dp.GradBuffer: backward writes grads into its views
+
+    def grad_sinks(self):
+        """Views of the flat gradient buffer to write into, or None.  Only used when every
+        parameter's .grad is None (autograd then adopts the views; if a .grad already existed it
+        would accumulate into an aliased buffer)."""
+        gb = self.gradbuf
+        if gb is None or any(p.grad is not None for p in self.params):
+            return None
+        return [gb.view_for(p) for p in self.params]
+
+    # -------------------------------------------------------------------------------- forward
+    def forward(self, x, params, save):
+        it = iter(params)
+        nxt = lambda: (next(it), next(it))  # noqa: E731
+        D = self.depth
+        pk = self.packs
+        s = {"x": x}
+        w, b = nxt(); t = conv3x3(x, w, b, pk); s["inc.t"] = t
+        w, b = nxt(); y = conv3x3(t, w, b, pk)
+        skips = [y]
+        for i in range(1, D):
+            p = K.maxpool2_fwd(skips[-1]); s["down%d.p" % i] = p
+            w, b = nxt(); t = conv3x3(p, w, b, pk); s["down%d.t" % i] = t
+            w, b = nxt(); y = conv3x3(t, w, b, pk)
+            skips.append(y)
+        s["skips"] = skips
+        y = skips[-1]
+        for j in range(1, D):
+            skip = skips[D - 1 - j]
+            w, b = nxt(); u = convT2x2(y, w, b, pk); s["up%d.u" % j] = u
+            w, b = nxt(); t = conv3x3(skip, w, b, pk, x1=u); s["up%d.t" % j] = t
+            w, b = nxt(); y = conv3x3(t, w, b, pk)
+            s["up%d.y" % j] = y
+        w, b = nxt()
+        logits = K.outconv_fwd(y, w.reshape(-1), b)
+        return logits, (s if save else None)
+
+    # ------------------------------------------------------------------------------- backward
+    def backward(self, s, dlogits, params):
+        D = self.depth
+        pk = self.packs
+        P = list(params)
+        grads = [None] * len(P)
+        sink = self.grad_sinks()
+        out = (lambda i: None) if sink is None else (lambda i: (sink[i], sink[i + 1]))  # noqa: E731
+        # parameter slots (see __init__ order)
+        n_enc = 4 * D
+        up_base = lambda j: n_enc + 6 * (j - 1)  # noqa: E731
+        outc = n_enc + 6 * (D - 1)
+        skips = s["skips"]
+
+        y_last = s["up%d.y" % (D - 1)]
+        o = out(outc)
+        g, dwo, dbo = K.outconv_bwd(y_last, P[outc].reshape(-1), dlogits, relu_mask=True,
+                                    out=None if o is None else (o[0].view(-1), o[1]))
+        grads[outc] = dwo.view_as(P[outc])
+        grads[outc + 1] = dbo
+
+        gskip = [None] * (D - 1)
+        for j in range(D - 1, 0, -1):
+            base = up_base(j)
+            t = s["up%d.t" % j]
+            u = s["up%d.u" % j]
+            skip = skips[D - 1 - j]
+            y_prev = skips[D - 1] if j == 1 else s["up%d.y" % (j - 1)]
+            # conv1 of up_j: y_j = relu(conv(t));  g = dZ
+            grads[base + 4], grads[base + 5] = conv3x3_wgrad(g, t, out=out(base + 4))
+            dt, _ = conv3x3_dgrad(g, P[base + 4], pk, mask0=t)
+            # conv0 over [skip | u]
+            grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, skip, u, out=out(base + 2))
+            cs = skip.shape[3]
+            dskip, du = conv3x3_dgrad(dt, P[base + 2], pk, split=cs, mask0=skip)
+            gskip[D - 1 - j] = dskip
+            # ConvT
+            grads[base], grads[base + 1] = convT2x2_wgrad(y_prev, du, out=out(base))
+            g = convT2x2_dgrad(du, P[base], pk, mask=y_prev)
+
+        for i in range(D - 1, 0, -1):
+            base = 4 * i
+            t = s["down%d.t" % i]
+            p = s["down%d.p" % i]
+            grads[base + 2], grads[base + 3] = conv3x3_wgrad(g, t, out=out(base + 2))
+            dt, _ = conv3x3_dgrad(g, P[base + 2], pk, mask0=t)
+            grads[base], grads[base + 1] = conv3x3_wgrad(dt, p, out=out(base))
+            dp, _ = conv3x3_dgrad(dt, P[base], pk)
+            g = K.maxpool2_bwd(skips[i - 1], dp, gskip[i - 1], relu_mask=True, accumulate=True)
+
+        t = s["inc.t"]
+        grads[2], grads[3] = conv3x3_wgrad(g, t, out=out(2))
+        dt, _ = conv3x3_dgrad(g, P[2], pk, mask0=t)
+        grads[0], grads[1] = conv3x3_wgrad(dt, s["x"], out=out(0))
+        return grads
+
+
+class TrunkFunction(torch.autograd.Function):
+    """autograd node: (trunk, save, x NCHW, *trunk params) -> logits [B,H,W]."""
+
+    @staticmethod
+    def forward(ctx, trunk, save, x, *params):
+        # ``save`` is decided by the caller: grad mode is always off inside Function.forward
+        xin = as_nhwc_input(x.detach())
+        detached = [p.detach() for p in params]
+        logits, saved = trunk.forward(xin, detached, save)
+        ctx.trunk = trunk
+        ctx.saved_acts = saved
+        ctx.params = detached
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        if ctx.saved_acts is None:
+            raise RuntimeError("trunk activations were not saved (forward ran without grad)")
+        grads = ctx.trunk.backward(ctx.saved_acts, dlogits.contiguous(), ctx.params)
+        ctx.saved_acts = None
+        return (None, None, None) + tuple(grads)

@@ -1,0 +1,2 @@
+from .unet_p import UNetp  # noqa: F401
+from .unet_p_res import UNetpRes  # noqa: F401

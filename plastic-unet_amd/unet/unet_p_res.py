@@ -1,0 +1,110 @@
+"""UNetpRes - drop-in for yaricom/Plastic-UNet ``src/unet/unet_p_res.py`` (module tree / state_dict
+compatible; constructor signature and defaults unchanged).
+
+The residual trunk's MI355X kernels (residual-add epilogue, ConvTranspose2d 3x3 s2 + crop,
+Dropout2d) are the next row of SURVEY.md section 8; until they land, forward() raises instead of
+silently falling back to ATen.
+"""
+import torch
+import torch.nn as nn
+
+__all__ = ["UNetpRes"]
+
+
+class conv_module(nn.Module):  # unet_p_res.py:142-164
+    def __init__(self, out_ch, kernel_size, stride=1, padding=1, activation=True, batch_norm=False):
+        super().__init__()
+        conv = nn.Conv2d(out_ch, out_ch, kernel_size=kernel_size, stride=stride, padding=padding)
+        self.conv = nn.Sequential(conv, nn.BatchNorm2d(out_ch)) if batch_norm else conv
+        self.activation = activation
+        if activation:
+            self.activ = nn.ReLU(inplace=True)
+
+
+class residual_block(nn.Module):  # unet_p_res.py:166-189
+    def __init__(self, out_ch, batch_norm=False):
+        super().__init__()
+        layers = [nn.ReLU(inplace=True)]
+        if batch_norm:
+            layers.append(nn.BatchNorm2d(out_ch))
+        layers += [conv_module(out_ch, kernel_size=3), conv_module(out_ch, kernel_size=3, activation=False)]
+        self.conv = nn.Sequential(*layers)
+
+
+class outconv(nn.Module):  # unet_p_res.py:191-198
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.conv = nn.Conv2d(in_ch, out_ch, kernel_size=1)
+
+
+def _stack(in_ch, out_ch, batch_norm):
+    return nn.Sequential(nn.Conv2d(in_ch, out_ch, kernel_size=3, padding=1),
+                         residual_block(out_ch=out_ch, batch_norm=batch_norm),
+                         residual_block(out_ch=out_ch, batch_norm=batch_norm), nn.ReLU(inplace=True))
+
+
+class middle(nn.Module):  # unet_p_res.py:223-238
+    def __init__(self, in_ch, out_ch, batch_norm=False):
+        super().__init__()
+        self.mconv = _stack(in_ch, out_ch, batch_norm)
+
+
+class down(nn.Module):  # unet_p_res.py:256-272
+    def __init__(self, in_ch, out_ch, batch_norm=False):
+        super().__init__()
+        self.dconv = _stack(in_ch, out_ch, batch_norm)
+
+
+class pool_drop(nn.Module):  # unet_p_res.py:240-253
+    def __init__(self, dropout_ratio):
+        super().__init__()
+        self.dpool = nn.Sequential(nn.MaxPool2d(2), nn.Dropout2d(p=dropout_ratio, inplace=True))
+
+
+class up(nn.Module):  # unet_p_res.py:200-220
+    def __init__(self, in_ch, out_ch, dropout_ratio, batch_norm=False):
+        super().__init__()
+        self.dconv = nn.ConvTranspose2d(in_ch, out_ch, kernel_size=3, stride=2, padding=0)
+        self.uconv = nn.Sequential(nn.Dropout2d(p=dropout_ratio, inplace=True), middle(in_ch, out_ch, batch_norm=False))
+
+
+class UNetpRes(nn.Module):
+    def __init__(self, n_channels, n_classes, device, neurons=16, dropout_ratio=0.5, alfa_type='free', rule='hebb',
+                 nbf=128, batch_norm=False, bilinear_upsample=False):
+        super().__init__()
+        self.n_classes = n_classes
+        self.n_channels = n_channels
+        self.nbf = nbf
+        self.torch_dev = device
+        self.alfa_type = alfa_type
+        self.rule = rule
+        self.neurons = neurons
+        self.dropout_ratio = dropout_ratio
+        self.w = nn.Parameter(.01 * torch.randn(nbf, nbf), requires_grad=True)
+        self.alpha = nn.Parameter(.01 * torch.rand(nbf, nbf), requires_grad=True)
+        self.eta = nn.Parameter(.01 * torch.ones(1), requires_grad=True)
+        n = neurons
+        self.conv1 = down(n_channels, n, batch_norm=batch_norm)
+        self.pool1 = pool_drop(dropout_ratio=dropout_ratio / 2)
+        self.conv2 = down(n, n * 2, batch_norm=batch_norm)
+        self.pool2 = pool_drop(dropout_ratio=dropout_ratio)
+        self.conv3 = down(n * 2, n * 4, batch_norm=batch_norm)
+        self.pool3 = pool_drop(dropout_ratio=dropout_ratio)
+        self.conv4 = down(n * 4, n * 8, batch_norm=batch_norm)
+        self.pool4 = pool_drop(dropout_ratio=dropout_ratio)
+        self.mid = middle(n * 8, n * 16, batch_norm=batch_norm)
+        self.uconv4 = up(n * 16, n * 8, dropout_ratio=dropout_ratio, batch_norm=batch_norm)
+        self.uconv3 = up(n * 8, n * 4, dropout_ratio=dropout_ratio, batch_norm=batch_norm)
+        self.uconv2 = up(n * 4, n * 2, dropout_ratio=dropout_ratio, batch_norm=batch_norm)
+        self.uconv1 = up(n * 2, n * 1, dropout_ratio=dropout_ratio, batch_norm=batch_norm)
+        self.outc = outconv(neurons, n_classes)
+        self.to(device)
+        print("UNet plastic model with plastic rule [%s] initialized" % self.rule)
+
+    def forward(self, x, hebb):
+        raise NotImplementedError("UNetpRes on the MI355X path is the next build item (SURVEY.md 8f); "
+                                  "use UNetp (the C1-C3 configurations)")
+
+    def initialZeroHebb(self, batch=None):
+        shape = (self.nbf, self.nbf) if batch is None else (batch, self.nbf, self.nbf)
+        return torch.zeros(*shape, dtype=torch.float, device=self.torch_dev)

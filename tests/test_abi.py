@@ -1,0 +1,109 @@
+"""CPU checks of the drop-in boundary: the C-ABI library loads and exports every symbol that
+include/plastic_unet.h declares, argument validation fails loudly without touching the GPU, and
+the product refuses CPU tensors (no fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "plastic_unet.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pu_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from punet import _lib
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 20
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert set(names) == bound, set(names) ^ bound
+    for n in names:
+        assert getattr(lib, n) is not None
+    assert lib.pu_abi_version() == 1
+
+
+def test_invalid_arguments_return_errors_without_gpu():
+    from punet import _lib
+    lib = _lib.load()
+    a = _lib.ConvArgs()
+    rc = lib.pu_conv_igemm(ctypes.byref(a), None)
+    assert rc == -1
+    assert b"bad grid" in lib.pu_last_error()
+    w = _lib.WgradArgs()
+    assert lib.pu_wgrad_workspace_bytes(ctypes.byref(w)) == 0
+    assert lib.pu_trace_update(None, None, None, None, None, 1, 4, 7, None) == -1
+    with pytest.raises(RuntimeError, match="pu_plastic_fwd failed"):
+        _lib.check(lib.pu_plastic_fwd(ctypes.byref(_lib.PlasticArgs()), None), "pu_plastic_fwd")
+
+
+def test_header_structs_match_ctypes_layout():
+    """Field order/size of the ctypes mirrors (a mismatch would corrupt every launch)."""
+    from punet import _lib
+    src = open(HEADER).read()
+    for cname, py in [("pu_conv_args", _lib.ConvArgs), ("pu_wgrad_args", _lib.WgradArgs),
+                      ("pu_plastic_args", _lib.PlasticArgs), ("pu_plastic_bwd_args", _lib.PlasticBwdArgs),
+                      ("pu_adam_tensor", _lib.AdamTensor)]:
+        body = dict((n, b) for b, n in re.findall(r"typedef struct \{([^}]*)\}\s*(\w+);", src))[cname]
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            decl = re.sub(r"\bconst\b", "", decl)
+            for part in decl.split(","):
+                fields.append(re.sub(r"[\*\s]", " ", part).split()[-1])
+        assert fields == [f for f, _ in py._fields_], (cname, fields)
+
+
+def test_product_refuses_cpu_tensors():
+    from unet import UNetp
+    net = UNetp(1, 1, torch.device("cpu"), nbf=32)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        net(torch.zeros(1, 1, 32, 32), torch.zeros(32, 32))
+
+
+def test_reference_batch_rule_kept():
+    from unet import UNetp
+    net = UNetp(1, 1, torch.device("cpu"), nbf=32)
+    with pytest.raises(ValueError, match="Only batch size: 1 is supported, but was: 2"):
+        net(torch.zeros(2, 1, 32, 32), torch.zeros(32, 32))
+
+
+def test_state_dict_and_init_match_reference_keys():
+    import oracle
+    from unet import UNetp, UNetpRes
+    torch.manual_seed(0)
+    a = UNetp(1, 1, torch.device("cpu"), rule="oja", nbf=64)
+    torch.manual_seed(0)
+    b = oracle.RefUNetp(1, 1, rule="oja", nbf=64)
+    sa, sb = a.state_dict(), b.state_dict()
+    assert list(sa) == list(sb)
+    assert all(torch.equal(sa[k], sb[k]) for k in sa)
+    torch.manual_seed(5)
+    a = UNetpRes(1, 1, torch.device("cpu"), neurons=4, nbf=101)
+    torch.manual_seed(5)
+    b = oracle.RefUNetpRes(1, 1, neurons=4, nbf=101)
+    assert list(a.state_dict()) == list(b.state_dict())
+    assert all(torch.equal(a.state_dict()[k], b.state_dict()[k]) for k in a.state_dict())
+
+
+def test_trunk_parameter_order_covers_every_trunk_parameter():
+    from unet import UNetp
+    from punet.trunk import UNetpTrunk
+    for depth, base in [(5, 8), (4, 16), (5, 64)]:
+        m = UNetp(1, 1, torch.device("cpu"), depth=depth, base_ch=base, nbf=64)
+        t = UNetpTrunk(m)
+        trunk = {id(p) for p in t.params}
+        head = {id(m.w), id(m.alpha), id(m.eta)}
+        assert trunk | head == {id(p) for p in m.parameters()}
+        assert len(t.params) == 4 * depth + 6 * (depth - 1) + 2

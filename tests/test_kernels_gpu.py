@@ -1,0 +1,253 @@
+"""Per-kernel parity of the HIP library against plain PyTorch-CPU fp32 (the oracle's arithmetic).
+
+Every call goes through the C-ABI (punet.kernels -> libplastic_unet.so).  Tolerances are fp32
+summation-order tolerances: rtol 1e-4 / atol 1e-5 relative to the output scale.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from punet import kernels as K  # noqa: E402
+from punet import trunk as T  # noqa: E402
+from punet.head import PlasticHeadFunction, bce_loss  # noqa: E402
+from punet.optim import FusedAdam  # noqa: E402
+import oracle  # noqa: E402
+from conftest import golden  # noqa: E402
+
+DEV = "cuda"
+
+
+def rnd(*shape, g, scale=1.0):
+    return (torch.randn(*shape, generator=g) * scale).float()
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def assert_close(got, ref, rtol=1e-4, atol_rel=1e-5):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    scale = max(ref.abs().max().item(), 1e-30)
+    torch.testing.assert_close(got, ref, rtol=rtol, atol=atol_rel * scale)
+
+
+CONV_CASES = [
+    # B, H, W, c0, c1, cout
+    (2, 16, 16, 1, 0, 8),       # stem: scalar loader
+    (2, 12, 20, 8, 0, 16),      # vec4 loader, non-square
+    (3, 16, 16, 64, 0, 64),     # chunk16 loader, 256x64 tile
+    (2, 8, 8, 16, 16, 24),      # two sources (concat), N not a tile multiple
+    (1, 8, 8, 8, 8, 8),         # two sources, vec4
+    (2, 32, 32, 32, 0, 128),    # 128x128 tile
+    (1, 4, 4, 64, 64, 40),      # tiny M, 64x64 tile
+]
+
+
+@pytest.mark.parametrize("B,H,W,c0,c1,cout", CONV_CASES)
+def test_conv3x3_fwd_dgrad_wgrad(B, H, W, c0, c1, cout):
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + c0 + c1 + cout)
+    x0 = rnd(B, c0, H, W, g=g)
+    x1 = rnd(B, c1, H, W, g=g) if c1 else None
+    w = rnd(cout, c0 + c1, 3, 3, g=g, scale=0.2)
+    b = rnd(cout, g=g)
+    xcat = torch.cat([x0, x1], 1) if c1 else x0
+    xcat.requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    z = F.conv2d(xcat, wr, br, padding=1)
+    y = torch.relu(z)
+    gy = rnd(*y.shape, g=g)
+    y.backward(gy)
+    dz = gy * (y > 0).float()
+
+    pk = T._Packs()
+    dx0, dx1 = nhwc(x0).to(DEV), (nhwc(x1).to(DEV) if c1 else None)
+    yk = T.conv3x3(dx0, w.to(DEV), b.to(DEV), pk, x1=dx1, relu=True)
+    assert_close(nchw(yk), y)
+    # dgrad (with the split + the relu masks of the sources)
+    dzk = nhwc(dz).to(DEV)
+    m0 = dx0
+    d0, d1 = T.conv3x3_dgrad(dzk, w.to(DEV), pk, split=c0 if c1 else None, mask0=m0,
+                             mask1=dx1 if c1 else None)
+    ref_dx = xcat.grad * (xcat > 0).float()
+    got = torch.cat([d0, d1], 3) if c1 else d0
+    assert_close(nchw(got), ref_dx)
+    # wgrad + bias grad
+    dw, db = T.conv3x3_wgrad(dzk, dx0, dx1)
+    assert_close(dw, wr.grad)
+    assert_close(db, br.grad)
+
+
+@pytest.mark.parametrize("B,h,cin,cout", [(2, 4, 16, 16), (3, 8, 64, 64), (2, 8, 8, 8), (1, 16, 128, 128)])
+def test_convT2x2(B, h, cin, cout):
+    g = torch.Generator().manual_seed(h * 7 + cin)
+    x = rnd(B, cin, h, h, g=g).relu().requires_grad_(True)
+    w = rnd(cin, cout, 2, 2, g=g, scale=0.3).requires_grad_(True)
+    b = rnd(cout, g=g).requires_grad_(True)
+    u = F.conv_transpose2d(x, w, b, stride=2)
+    gu = rnd(*u.shape, g=g)
+    u.backward(gu)
+    pk = T._Packs()
+    xk = nhwc(x.detach()).to(DEV)
+    uk = T.convT2x2(xk, w.detach().to(DEV), b.detach().to(DEV), pk)
+    assert_close(nchw(uk), u)
+    guk = nhwc(gu).to(DEV)
+    dxk = T.convT2x2_dgrad(guk, w.detach().to(DEV), pk, mask=xk)
+    assert_close(nchw(dxk), x.grad * (x > 0).float())
+    dw, db = T.convT2x2_wgrad(xk, guk)
+    assert_close(dw, w.grad)
+    assert_close(db, b.grad)
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 8, 8, 16), (1, 7, 9, 3), (2, 16, 16, 64)])
+def test_maxpool(B, H, W, C):
+    g = torch.Generator().manual_seed(H * W + C)
+    x = rnd(B, C, H, W, g=g).relu()
+    x[:, :, 0:2, 0:2] = 0.5            # ties inside one window: first max wins
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 2)
+    gy = rnd(*y.shape, g=g)
+    y.backward(gy)
+    xk = nhwc(x).to(DEV)
+    yk = K.maxpool2_fwd(xk)
+    assert torch.equal(nchw(yk).cpu(), y.detach())
+    prev = rnd(B, C, H, W, g=g)
+    dxk = nhwc(prev).to(DEV)
+    K.maxpool2_bwd(xk, nhwc(gy).to(DEV), dxk, relu_mask=True, accumulate=True)
+    ref = prev + xr.grad * (x > 0).float()
+    assert_close(nchw(dxk), ref, rtol=1e-6, atol_rel=1e-7)
+    dxk2 = torch.empty_like(xk)
+    K.maxpool2_bwd(xk, nhwc(gy).to(DEV), dxk2, relu_mask=False, accumulate=False)
+    assert torch.equal(nchw(dxk2).cpu(), xr.grad)
+
+
+@pytest.mark.parametrize("rows_hw,C", [((2, 16, 16), 64), ((1, 8, 8), 8), ((3, 5, 7), 128)])
+def test_outconv(rows_hw, C):
+    B, H, W = rows_hw
+    g = torch.Generator().manual_seed(C + H)
+    x = rnd(B, C, H, W, g=g).relu().requires_grad_(True)
+    w = rnd(1, C, 1, 1, g=g).requires_grad_(True)
+    b = rnd(1, g=g).requires_grad_(True)
+    y = F.conv2d(x, w, b)
+    gy = rnd(*y.shape, g=g)
+    y.backward(gy)
+    xk = nhwc(x.detach()).to(DEV)
+    yk = K.outconv_fwd(xk, w.detach().reshape(-1).to(DEV), b.detach().to(DEV))
+    assert_close(yk, y[:, 0])
+    dxk, dwk, dbk = K.outconv_bwd(xk, w.detach().reshape(-1).to(DEV), gy[:, 0].contiguous().to(DEV), relu_mask=True)
+    assert_close(nchw(dxk), x.grad * (x > 0).float())
+    assert_close(dwk, w.grad.reshape(-1))
+    assert_close(dbk, b.grad)
+
+
+@pytest.mark.parametrize("rule", ["hebb", "oja"])
+@pytest.mark.parametrize("N", [32, 128])
+def test_plastic_head_golden(rule, N):
+    g = golden("head_%s_N%d.npz" % (rule, N))
+    t = {k: torch.from_numpy(v) for k, v in g.items()}
+    X = t["X"][None].to(DEV).requires_grad_(True)
+    w = t["w"].to(DEV).requires_grad_(True)
+    al = t["alpha"].to(DEV).requires_grad_(True)
+    eta = t["eta"].to(DEV).requires_grad_(True)
+    Y, Hn = PlasticHeadFunction.apply(X, t["H"][None].to(DEV), w, al, eta, 0 if rule == "hebb" else 1, True)
+    loss = bce_loss(Y, t["t"].to(DEV))
+    loss.backward()
+    assert_close(Y[0], t["Y"])
+    assert_close(Hn[0], t["Hn"])
+    assert abs(loss.item() - float(g["loss"])) <= 1e-6 * abs(float(g["loss"]))
+    assert_close(X.grad[0], t["dX"])
+    assert_close(w.grad, t["dw"])
+    assert_close(al.grad, t["dalpha"])
+    assert eta.grad is None          # S3
+
+
+@pytest.mark.parametrize("rule", ["hebb", "oja"])
+def test_trace_update_bit_exact(rule):
+    """Elementwise update: same op order as ATen, FP contraction off -> bit-identical to the oracle."""
+    g = torch.Generator().manual_seed(3)
+    B, N = 32, 128
+    H = rnd(B, N, N, g=g, scale=0.3)
+    X = rnd(B, N, N, g=g, scale=2.0)
+    Y = torch.rand(B, N, N, generator=g)
+    eta = torch.tensor([0.0137])
+    ref = oracle.trace_update(H, X[:, 0, :], Y[:, 0, :], eta, rule)
+    got = K.trace_update(H.to(DEV), X.to(DEV), Y.to(DEV), eta.to(DEV), 0 if rule == "hebb" else 1)
+    assert torch.equal(got.cpu(), ref)
+
+
+@pytest.mark.parametrize("rule", ["hebb", "oja"])
+def test_trace_sequence_golden(rule):
+    g = golden("trace_seq_%s.npz" % rule)
+    w, al, eta = (torch.from_numpy(g[k]).to(DEV) for k in ("w", "alpha", "eta"))
+    H = torch.zeros(1, 32, 32, device=DEV)
+    for k in range(16):
+        Y, H = K.plastic_fwd(torch.from_numpy(g["X"][k])[None].to(DEV), H, w, al, eta, 0 if rule == "hebb" else 1)
+        assert_close(Y[0], torch.from_numpy(g["Y"][k]))
+        assert_close(H[0], torch.from_numpy(g["H"][k]))
+
+
+def test_plastic_head_batched_slots_match_oracle():
+    g = torch.Generator().manual_seed(9)
+    B, N = 32, 128
+    X = rnd(B, N, N, g=g, scale=2.0).requires_grad_(True)
+    H = rnd(B, N, N, g=g, scale=0.2)
+    w = rnd(N, N, g=g, scale=0.05).requires_grad_(True)
+    al = (torch.rand(N, N, generator=g) * 0.05).requires_grad_(True)
+    eta = torch.tensor([0.02])
+    tg = (torch.rand(B, N, N, generator=g) > 0.5).float()
+    Y, Hn = oracle.plastic_head(X, H, w, al, eta, "oja")
+    oracle.bce_loss(Y, tg).backward()
+    Xd = X.detach().to(DEV).requires_grad_(True)
+    wd = w.detach().to(DEV).requires_grad_(True)
+    ad = al.detach().to(DEV).requires_grad_(True)
+    Yk, Hk = PlasticHeadFunction.apply(Xd, H.to(DEV), wd, ad, eta.to(DEV), 1, True)
+    bce_loss(Yk, tg.to(DEV)).backward()
+    assert_close(Yk, Y)
+    assert_close(Hk, Hn)
+    assert_close(Xd.grad, X.grad)
+    assert_close(wd.grad, w.grad)
+    assert_close(ad.grad, al.grad)
+
+
+def test_bce_edges_golden():
+    g = golden("bce_edge.npz")
+    y = torch.from_numpy(g["y"]).to(DEV).requires_grad_(True)
+    loss = bce_loss(y, torch.from_numpy(g["t"]).to(DEV))
+    loss.backward()
+    assert abs(loss.item() - float(g["loss"])) <= 1e-6 * abs(float(g["loss"]))
+    assert_close(y.grad, torch.from_numpy(g["dy"]))
+    z = torch.from_numpy(g["z"]).to(DEV).requires_grad_(True)
+    lz = bce_loss(torch.sigmoid(z), torch.from_numpy(g["tz"]).to(DEV))
+    lz.backward()
+    assert abs(lz.item() - float(g["lz"])) <= 1e-6 * abs(float(g["lz"]))
+    assert_close(z.grad, torch.from_numpy(g["dz"]))
+
+
+def test_fused_adam_matches_torch_adam():
+    g = torch.Generator().manual_seed(1)
+    shapes = [(64, 3, 3, 3), (64,), (7,), (1000, 33), (5, 5)]
+    ref = [torch.nn.Parameter(rnd(*s, g=g)) for s in shapes]
+    dev = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ref]
+    o1 = torch.optim.Adam(ref, lr=3e-3)
+    o2 = FusedAdam(dev, lr=3e-3)
+    s1 = torch.optim.lr_scheduler.StepLR(o1, step_size=2, gamma=0.666)
+    s2 = torch.optim.lr_scheduler.StepLR(o2, step_size=2, gamma=0.666)
+    for step in range(5):
+        for a, b in zip(ref, dev):
+            gr = rnd(*a.shape, g=g)
+            a.grad = gr.clone()
+            b.grad = gr.to(DEV)
+        dev[2].grad = None      # a parameter without gradient is skipped (eta, S3)
+        ref[2].grad = None
+        o1.step(); o2.step(); s1.step(); s2.step()
+    for a, b in zip(ref, dev):
+        assert_close(b, a, rtol=1e-6, atol_rel=1e-6)
