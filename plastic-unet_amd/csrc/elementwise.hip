@@ -235,14 +235,23 @@ __global__ void outconv_bwd_kernel(const float* __restrict__ x, const float* __r
     }
 }
 
+// one block per column: fixed-order fp64 tree over the per-block partials
 __global__ void column_sum_kernel(const float* __restrict__ partial, int nparts, int cols, float* __restrict__ dw,
                                   float* __restrict__ db) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c > cols) return;
-    float s = 0.f;
-    for (int q = 0; q < nparts; ++q) s += partial[(long long)q * (cols + 1) + c];
-    if (c < cols) dw[c] = s;
-    else db[0] = s;
+    __shared__ double red[256];
+    const int c = blockIdx.x;
+    double s = 0.0;
+    for (int q = threadIdx.x; q < nparts; q += 256) s += partial[(long long)q * (cols + 1) + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (c < cols) dw[c] = (float)red[0];
+        else db[0] = (float)red[0];
+    }
 }
 
 static int grid_for(long long total, int block = 256, int cap = 8192) {
@@ -343,7 +352,6 @@ extern "C" int pu_outconv_bwd(const float* x, const float* w, const float* dy, f
     float* part = (float*)workspace;
     hipLaunchKernelGGL(outconv_bwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, w, dy, dx, part, rows, c,
                        relu_mask);
-    hipLaunchKernelGGL(column_sum_kernel, dim3((c + 1 + 255) / 256), dim3(256), 0, as_stream(stream), part, blocks, c,
-                       dw, db);
+    hipLaunchKernelGGL(column_sum_kernel, dim3(c + 1), dim3(256), 0, as_stream(stream), part, blocks, c, dw, db);
     return check_launch("pu_outconv_bwd");
 }

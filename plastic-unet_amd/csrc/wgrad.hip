@@ -205,46 +205,63 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
     }
 }
 
-// Sum the per-split partials (fixed order) and scatter to [n][c][kh][kw] + bias.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Nr, int Kc, int N, int K,
-                                    int C, int kh, int kw, int bias_mode, float* __restrict__ dw,
-                                    float* __restrict__ db, int accumulate) {
+// Split-K reduction, pass 1: part[g][idx] = sum over splits z = g, g+G, ... of slab[z][idx]
+// (fp64, 4 independent accumulators so each thread keeps several loads in flight).
+__global__ void wgrad_sum_splits_kernel(const float* __restrict__ slab, int splits, long long total, int G,
+                                        double* __restrict__ part) {
+    const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int g = blockIdx.y;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int z = g;
+    for (; z + 3 * G < splits; z += 4 * G) {
+        s0 += slab[(long long)z * total + idx];
+        s1 += slab[(long long)(z + G) * total + idx];
+        s2 += slab[(long long)(z + 2 * G) * total + idx];
+        s3 += slab[(long long)(z + 3 * G) * total + idx];
+    }
+    for (; z < splits; z += G) s0 += slab[(long long)z * total + idx];
+    part[(long long)g * total + idx] = (s0 + s1) + (s2 + s3);
+}
+
+// pass 2: sum the G groups (fixed order) and scatter to PyTorch's [n][c][kh][kw] + bias.
+// Threads [0, total) handle slab entries; threads [total, total + C) the ConvT bias (mode 2).
+__global__ void wgrad_finish_kernel(const double* __restrict__ part, int G, int Nr, int Kc, int N, int K, int C,
+                                    int kh, int kw, int bias_mode, float* __restrict__ dw, float* __restrict__ db,
+                                    int accumulate) {
     const long long total = (long long)Nr * Kc;
-    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * blockDim.x) {
+    const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (idx < total) {
         const int n = int(idx / Kc);
         const int k = int(idx - (long long)n * Kc);
-        float s = 0.f;
-        for (int z = 0; z < splits; ++z) s += slab[(long long)z * total + idx];
-        if (n < N && k < K) {
+        if (n >= N) return;
+        double s = 0.0;
+        for (int g = 0; g < G; ++g) s += part[(long long)g * total + idx];
+        const float v = (float)s;
+        if (k < K) {
             const int tap = k / C, c = k - tap * C;
             const int r = tap / kw, ss = tap - r * kw;
             float* o = dw + (((long long)n * C + c) * kh + r) * kw + ss;
-            *o = accumulate ? *o + s : s;
-        } else if (bias_mode == 1 && n < N && k == K) {
-            db[n] = accumulate ? db[n] + s : s;
+            *o = accumulate ? *o + v : v;
+        } else if (bias_mode == 1 && k == K) {
+            db[n] = accumulate ? db[n] + v : v;
         }
+    } else if (bias_mode == 2 && idx < total + C) {
+        const int c = int(idx - total);
+        double s = 0.0;
+        for (int t = 0; t < kh * kw; ++t)
+            for (int g = 0; g < G; ++g) s += part[(long long)g * total + (long long)N * Kc + t * C + c];
+        const float v = (float)s;
+        db[c] = accumulate ? db[c] + v : v;
     }
-}
-
-// ConvT bias (bias_mode 2): db[c] = sum over taps of the ones-row partial sums
-__global__ void wgrad_bias_rows_kernel(const float* __restrict__ slab, int splits, int Nr, int Kc, int N, int C,
-                                       int taps, float* __restrict__ db, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const long long total = (long long)Nr * Kc;
-    float s = 0.f;
-    for (int t = 0; t < taps; ++t) {
-        float st = 0.f;
-        for (int z = 0; z < splits; ++z) st += slab[(long long)z * total + (long long)N * Kc + t * C + c];
-        s += st;
-    }
-    db[c] = accumulate ? db[c] + s : s;
 }
 
 struct WgradPlan {
-    int BN, BK, splits, mps, Nr, Kc, M, K, C;
+    int BN, BK, splits, mps, Nr, Kc, M, K, C, G;
     bool qvec;
+    size_t slab_bytes() const { return (size_t)splits * Nr * Kc * sizeof(float); }
+    size_t part_bytes() const { return (size_t)G * Nr * Kc * sizeof(double); }
+    size_t ws_bytes() const { return ((slab_bytes() + 255) / 256) * 256 + part_bytes(); }
 };
 
 static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
@@ -278,6 +295,7 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     int mps = ceil_div(ceil_div(M, splits), WG_BM) * WG_BM;
     pl->mps = mps;
     pl->splits = ceil_div(M, mps);
+    pl->G = pl->splits < 16 ? pl->splits : 16;
     return PU_OK;
 }
 
@@ -288,7 +306,7 @@ using namespace pu;
 extern "C" size_t pu_wgrad_workspace_bytes(const pu_wgrad_args* a) {
     WgradPlan pl;
     if (plan_wgrad(a, &pl) != PU_OK) return 0;
-    return (size_t)pl.splits * pl.Nr * pl.Kc * sizeof(float);
+    return pl.ws_bytes();
 }
 
 extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec, int* splits) {
@@ -306,7 +324,7 @@ extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes
     WgradPlan pl;
     int st = plan_wgrad(a, &pl);
     if (st != PU_OK) return st;
-    const size_t need = (size_t)pl.splits * pl.Nr * pl.Kc * sizeof(float);
+    const size_t need = pl.ws_bytes();
     if (!workspace || ws_bytes < need)
         return fail(PU_ERR_WORKSPACE, "pu_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
 
@@ -334,13 +352,12 @@ extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes
     if (st != PU_OK) return st;
 
     const long long total = (long long)pl.Nr * pl.Kc;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)workspace, pl.splits, pl.Nr,
-                       pl.Kc, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias, a->accumulate);
-    if (a->bias_mode == 2) {
-        hipLaunchKernelGGL(wgrad_bias_rows_kernel, dim3(ceil_div(pl.C, 256)), dim3(256), 0, s, (const float*)workspace,
-                           pl.splits, pl.Nr, pl.Kc, a->n, pl.C, a->kh * a->kw, a->dbias, a->accumulate);
-    }
+    double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
+    hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
+                       (const float*)workspace, pl.splits, total, pl.G, part);
+    const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
+    hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+                       (const double*)part, pl.G, pl.Nr, pl.Kc, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode,
+                       a->dweight, a->dbias, a->accumulate);
     return check_launch("pu_wgrad (reduce)");
 }

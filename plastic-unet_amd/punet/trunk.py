@@ -152,6 +152,7 @@ class UNetpTrunk:
                 self.params += [seq[idx].weight, seq[idx].bias]
         self.params += [model.outc.conv.weight, model.outc.conv.bias]
         self.gradbuf = None      # punet.dp.GradBuffer: backward writes grads into its views
+        self.debug = None        # dict: when set, backward stores each layer's dZ (tests/diagnostics)
 
     def grad_sinks(self):
         """Views of the flat gradient buffer to write into, or None.  Only used when every
@@ -217,6 +218,8 @@ class UNetpTrunk:
             u = s["up%d.u" % j]
             skip = skips[D - 1 - j]
             y_prev = skips[D - 1] if j == 1 else s["up%d.y" % (j - 1)]
+            if self.debug is not None:
+                self.debug["up%d.c1" % j] = g
             # conv1 of up_j: y_j = relu(conv(t));  g = dZ
             grads[base + 4], grads[base + 5] = conv3x3_wgrad(g, t, out=out(base + 4))
             dt, _ = conv3x3_dgrad(g, P[base + 4], pk, mask0=t)
@@ -224,6 +227,9 @@ class UNetpTrunk:
             grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, skip, u, out=out(base + 2))
             cs = skip.shape[3]
             dskip, du = conv3x3_dgrad(dt, P[base + 2], pk, split=cs, mask0=skip)
+            if self.debug is not None:
+                self.debug["up%d.c0" % j] = dt
+                self.debug["up%d.up" % j] = du
             gskip[D - 1 - j] = dskip
             # ConvT
             grads[base], grads[base + 1] = convT2x2_wgrad(y_prev, du, out=out(base))
@@ -233,16 +239,24 @@ class UNetpTrunk:
             base = 4 * i
             t = s["down%d.t" % i]
             p = s["down%d.p" % i]
+            if self.debug is not None:
+                self.debug["down%d.c1" % i] = g
             grads[base + 2], grads[base + 3] = conv3x3_wgrad(g, t, out=out(base + 2))
             dt, _ = conv3x3_dgrad(g, P[base + 2], pk, mask0=t)
             grads[base], grads[base + 1] = conv3x3_wgrad(dt, p, out=out(base))
+            if self.debug is not None:
+                self.debug["down%d.c0" % i] = dt
             dp, _ = conv3x3_dgrad(dt, P[base], pk)
             g = K.maxpool2_bwd(skips[i - 1], dp, gskip[i - 1], relu_mask=True, accumulate=True)
 
         t = s["inc.t"]
+        if self.debug is not None:
+            self.debug["inc.c1"] = g
         grads[2], grads[3] = conv3x3_wgrad(g, t, out=out(2))
         dt, _ = conv3x3_dgrad(g, P[2], pk, mask0=t)
         grads[0], grads[1] = conv3x3_wgrad(dt, s["x"], out=out(0))
+        if self.debug is not None:
+            self.debug["inc.c0"] = dt
         return grads
 
 
