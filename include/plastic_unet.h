@@ -66,6 +66,10 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
  *   cols k  = (tap r*kw+s, channel c) of the input at pixel (ho*stride-pad+r, wo*stride-pad+s),
  *             channels [0,c0) read from src0 and [c0,c0+c1) from src1 (concat without a copy)
  *   weight  = packed [n][k_pad] (pu_pack_weight), k_pad >= kh*kw*(c0+c1), k_pad % 16 == 0
+ *   cgroup  = K order of the packed weight: 0 -> k = tap*C + c (tap-major);  16 or 32 ->
+ *             k = (g*taps + tap)*cgroup + (c % cgroup), g = c / cgroup (channel-group-major: the
+ *             taps of one channel group are consecutive K stages, so their shifted re-reads of the
+ *             same pixels hit L2).  Requires c0 % cgroup == 0 and c1 % cgroup == 0.
  * Epilogue per element: v = acc (+ bias) ; RELU: v = max(v,0) ; mask: v *= (mask > 0) ;
  *   ACCUM: dst += v else dst = v.  Columns [0,n0) go to dst0 (NHWC, n0 channels), [n0,n) to
  *   dst1 (NHWC, n-n0 channels).  SHUFFLE2: n = (2i+j)*co + c is stored at pixel (2ho+i, 2wo+j)
@@ -80,7 +84,7 @@ typedef struct {
     int kh, kw, stride, pad;
     const float* src0; int c0;
     const float* src1; int c1;
-    const float* weight; int k_pad;
+    const float* weight; int k_pad; int cgroup;
     int n;
     const float* bias;
     float* dst0; int n0;
@@ -134,9 +138,10 @@ enum {
     PU_PACK_CONVT_FWD = 2,  /* w[I][O][R][S] -> p[(r*S+s)*O+o][i]                           */
     PU_PACK_CONVT_DGRAD = 3 /* w[I][O][R][S] -> p[i][(r*S+s)*O+o]                           */
 };
-/* d0,d1 = first two dims of w; rows of p are k_pad floats wide (zero padded) */
+/* d0,d1 = first two dims of w; rows of p are k_pad floats wide (zero padded).  cgroup != 0 packs
+ * the K axis channel-group-major (see pu_conv_args.cgroup) for the FWD/DGRAD/CONVT_DGRAD modes. */
 int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw,
-                   int k_pad, void* stream);
+                   int k_pad, int cgroup, void* stream);
 int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, void* stream);
 
 /* MaxPool2d(2) on NHWC (floor for odd sizes), first-max tie rule of ATen's CPU kernel.

@@ -66,4 +66,14 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 
 inline int ceil_div(long long a, long long b) { return int((a + b - 1) / b); }
 
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (block b runs on
+// XCD b % 8).  Map hardware block b to a logical tile so that each XCD gets one CONTIGUOUS range
+// of logical tiles (neighbouring tiles share input rows/halos -> reuse in that XCD's L2).
+// Bijective for any total (the ragged variant of cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_remap(int b, int total) {
+    const int xcd = b & 7, local = b >> 3;
+    const int q = total >> 3, r = total & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
 }  // namespace pu

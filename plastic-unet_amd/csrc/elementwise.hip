@@ -13,14 +13,24 @@ namespace pu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// K position -> tap-major index (tap*C + c) for a channel-group-major packed K axis
+__device__ __forceinline__ int ungroup_k(int k, int C, int taps, int G) {
+    if (G == 0 || k >= taps * C) return k;
+    const int tg = k / G, cg = k - tg * G;
+    const int g = tg / taps, tap = tg - g * taps;
+    return tap * C + g * G + cg;
+}
+
 __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restrict__ p, int mode, int d0, int d1,
-                                   int kh, int kw, int k_pad, int rows) {
+                                   int kh, int kw, int k_pad, int rows, int G) {
     const long long total = (long long)rows * k_pad;
     const int taps = kh * kw;
+    const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;   // channels along K (taps*Ck columns)
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * blockDim.x) {
         const int row = int(idx / k_pad);
-        const int k = int(idx - (long long)row * k_pad);
+        const int k = (mode == PU_PACK_CONVT_FWD) ? int(idx - (long long)row * k_pad)
+                                                   : ungroup_k(int(idx - (long long)row * k_pad), Ck, taps, G);
         float v = 0.f;
         if (mode == PU_PACK_CONV_FWD) {          // w[O=d0][I=d1][R][S] -> [o][(r*S+s)*I+i]
             if (k < taps * d1) {
@@ -266,8 +276,13 @@ static int grid_for(long long total, int block = 256, int cap = 8192) {
 using namespace pu;
 
 extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw, int k_pad,
-                              void* stream) {
+                              int cgroup, void* stream) {
     PU_REQUIRE(w && packed && d0 > 0 && d1 > 0 && kh > 0 && kw > 0 && k_pad > 0, "pu_pack_weight: bad args");
+    PU_REQUIRE(cgroup == 0 || cgroup == 16 || cgroup == 32, "pu_pack_weight: cgroup %d", cgroup);
+    if (cgroup) {
+        const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;
+        PU_REQUIRE(mode == PU_PACK_CONVT_FWD || Ck % cgroup == 0, "pu_pack_weight: %d channels not a multiple of cgroup %d", Ck, cgroup);
+    }
     PU_REQUIRE(mode >= 0 && mode <= 3, "pu_pack_weight: mode %d", mode);
     const int taps = kh * kw;
     int rows, kmin;
@@ -280,7 +295,7 @@ extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, i
     PU_REQUIRE(k_pad >= kmin, "pu_pack_weight: k_pad %d < %d", k_pad, kmin);
     const long long total = (long long)rows * k_pad;
     hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), w, packed, mode, d0,
-                       d1, kh, kw, k_pad, rows);
+                       d1, kh, kw, k_pad, rows, cgroup);
     return check_launch("pu_pack_weight");
 }
 

@@ -13,6 +13,13 @@
 // A[i][kk*8 + 4h + s] and B[kk*8 + 4h + s][j] - the same k on both operands, so the sum is exact.
 #include "common.h"
 
+// Experimental ablations for performance analysis (tools/ablate.sh); 0 in the product build.
+//   1: no global loads in the K loop (LDS tiles keep stale data)   2: no LDS staging stores
+//   3: 1 + 2 (LDS reads + MFMA + barrier only)                      4: 3 without the barrier
+#ifndef PU_ABLATE
+#define PU_ABLATE 0
+#endif
+
 namespace pu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -25,7 +32,7 @@ enum { LOAD_CHUNK16 = 0, LOAD_VEC4 = 1, LOAD_SCALAR = 2 };
 
 struct IgemmParams {
     int M, N, K, k_pad;
-    int Hi, Wi, Ho, Wo, kw, stride, pad;
+    int Hi, Wi, Ho, Wo, kh, kw, stride, pad;
     int C, c0, c1;
     const float* src0;
     const float* src1;
@@ -36,7 +43,9 @@ struct IgemmParams {
     const float* mask0;
     const float* mask1;
     int n0, flags;
-    FastDiv dWo, dHo, dC, dKw, dCo;
+    int cgroup, taps, gn;   // K order (0 tap-major, 16/32 channel-group-major), kh*kw, n-blocks
+    int vec_epi;            // float4 epilogue (channel counts % 4 == 0, 16-byte aligned buffers)
+    FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
 };
 
 // Load 4 consecutive k values (k, k+1, k+2, k+3) of GEMM row (pb, hb, wb) into v.
@@ -95,15 +104,24 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
     const int wave = tid >> 6;
     const int wm = wave % WM, wn = wave / WM;
     const int lr = lane & 31, lh = lane >> 5;
-    const int m_blk = blockIdx.x * BM;
-    const int n_blk = blockIdx.y * BN;
+    // XCD-aware tile order: each XCD walks a contiguous range of (m-block, all n-blocks)
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mb = tile / p.gn;
+    const int m_blk = mb * BM;
+    const int n_blk = (tile - mb * p.gn) * BN;
 
-    // ---- per-thread A rows: row = (tid >> 2) + 64*i, k-quad = tid & 3
-    const int kq = tid & 3;
+    // ---- loader mapping: lane -> row (lane & 15) + 16*wave (+ 64*i), 16-byte k-quad lane >> 4.
+    // 8 consecutive lanes write one k-quad of 8 different rows (row stride 20 floats): the
+    // ds_write_b128 lane groups touch 8 distinct 4-bank slots, so staging is conflict-free.
+    const int kq = lane >> 4;
+    const int lrow = (lane & 15) + 16 * wave;
     int pb[A_LD], hb[A_LD], wb[A_LD];
+    long long rb0[A_LD], rb1[A_LD];   // element offset of the tap-(0,0) pixel in src0 / src1
+    unsigned tmask[A_LD];             // bit (r*kw+s): that tap's input pixel lies inside the image
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
-        int m = m_blk + (tid >> 2) + 64 * i;
+        int m = m_blk + lrow + 64 * i;
+        pb[i] = 0; hb[i] = -(1 << 28); wb[i] = 0; tmask[i] = 0; rb0[i] = 0; rb1[i] = 0;
         if (m < p.M) {
             int t = fdiv(m, p.dWo);
             int wo = m - t * p.Wo;
@@ -112,17 +130,24 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
             pb[i] = b * p.Hi * p.Wi;
             hb[i] = ho * p.stride - p.pad;
             wb[i] = wo * p.stride - p.pad;
-        } else {
-            pb[i] = 0;
-            hb[i] = -(1 << 28);  // fails the bounds test -> zeros
-            wb[i] = 0;
+            if (MODE == LOAD_CHUNK16) {
+                long long pix0 = (long long)pb[i] + (long long)hb[i] * p.Wi + wb[i];
+                rb0[i] = pix0 * p.c0;
+                rb1[i] = pix0 * p.c1;
+                unsigned msk = 0;
+                for (int r = 0; r < p.kh; ++r)
+                    for (int q = 0; q < p.kw; ++q)
+                        if ((unsigned)(hb[i] + r) < (unsigned)p.Hi && (unsigned)(wb[i] + q) < (unsigned)p.Wi)
+                            msk |= 1u << (r * p.kw + q);
+                tmask[i] = msk;
+            }
         }
     }
     const float* wrow[B_LD];
     bool wok[B_LD];
 #pragma unroll
     for (int i = 0; i < B_LD; ++i) {
-        int n = n_blk + (tid >> 2) + 64 * i;
+        int n = n_blk + lrow + 64 * i;
         wok[i] = n < p.N;
         wrow[i] = p.wt + (long long)(wok[i] ? n : 0) * p.k_pad + kq * 4;
     }
@@ -131,24 +156,32 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
     auto load_stage = [&](int t) {
         const int k0 = t * IG_BK;
         if (MODE == LOAD_CHUNK16) {
-            // the whole 16-wide k chunk shares one tap and one source (c0, c1 multiples of 16)
-            int tap = fdiv(k0, p.dC);
-            int c = k0 - tap * p.C;
-            int r = fdiv(tap, p.dKw);
-            int s = tap - r * p.kw;
-            bool first = c < p.c0;
+            // the whole 16-wide k chunk shares one tap and one source (c0, c1 multiples of 16):
+            // tap/source/offset are wave-uniform, each row only tests its tap bit and adds its base
+            int tap, c;
+            if (p.cgroup) {
+                // channel-group-major: stage t covers group g, tap, and 16-channel half h
+                const int per = p.cgroup >> 4;                // stages per (group, tap)
+                const int tg = per == 2 ? (t >> 1) : t;
+                const int h = per == 2 ? (t & 1) : 0;
+                const int g = fdiv(tg, p.dTaps);
+                tap = tg - g * p.taps;
+                c = g * p.cgroup + h * 16;
+            } else {
+                tap = fdiv(k0, p.dC);
+                c = k0 - tap * p.C;
+            }
+            const int r = fdiv(tap, p.dKw);
+            const int s = tap - r * p.kw;
+            const bool first = c < p.c0;
             const float* src = first ? p.src0 : p.src1;
-            int cs = first ? p.c0 : p.c1;
-            int cc = (first ? c : c - p.c0) + kq * 4;
-            bool kin = k0 < p.K;
+            const int cs = first ? p.c0 : p.c1;
+            const long long off = (long long)(r * p.Wi + s) * cs + (first ? c : c - p.c0) + kq * 4;
+            const unsigned bit = (k0 < p.K) ? (1u << tap) : 0u;
 #pragma unroll
             for (int i = 0; i < A_LD; ++i) {
-                int hi = hb[i] + r, wi = wb[i] + s;
                 f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (kin && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi) {
-                    long long pix = (long long)pb[i] + hi * p.Wi + wi;
-                    v = *reinterpret_cast<const f32x4*>(src + pix * cs + cc);
-                }
+                if (tmask[i] & bit) v = *reinterpret_cast<const f32x4*>(src + (first ? rb0[i] : rb1[i]) + off);
                 ra[i] = v;
             }
         } else {
@@ -167,10 +200,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
         float* b = Bs + buf * BN * IG_LDS;
 #pragma unroll
         for (int i = 0; i < A_LD; ++i)
-            *reinterpret_cast<f32x4*>(a + ((tid >> 2) + 64 * i) * IG_LDS + kq * 4) = ra[i];
+            *reinterpret_cast<f32x4*>(a + (lrow + 64 * i) * IG_LDS + kq * 4) = ra[i];
 #pragma unroll
         for (int i = 0; i < B_LD; ++i)
-            *reinterpret_cast<f32x4*>(b + ((tid >> 2) + 64 * i) * IG_LDS + kq * 4) = rb[i];
+            *reinterpret_cast<f32x4*>(b + (lrow + 64 * i) * IG_LDS + kq * 4) = rb[i];
     };
 
     f32x16 acc[FM][FN];
@@ -191,7 +224,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
 
     for (int t = 0; t < T; ++t) {
         const int buf = t & 1;
-        if (t + 1 < T) load_stage(t + 1);
+        if (PU_ABLATE != 1 && PU_ABLATE < 3 && t + 1 < T) load_stage(t + 1);
         const float* a = As + buf * BM * IG_LDS;
         const float* b = Bs + buf * BN * IG_LDS;
 #pragma unroll
@@ -209,64 +242,103 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
                     for (int j = 0; j < FN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+                        // weights as the MFMA A operand, pixels as B: acc[i][j] holds D^T (rows =
+                        // output channels), so each lane ends with 4 consecutive channels of a pixel
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
         }
-        if (t + 1 < T) store_stage(buf ^ 1);
-        __syncthreads();
+        if (PU_ABLATE != 2 && PU_ABLATE < 3 && t + 1 < T) store_stage(buf ^ 1);
+        if (PU_ABLATE != 4) __syncthreads();
     }
 
-    // ---- epilogue: C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+    // ---- epilogue.  acc[i][j] = D^T block: MFMA row = channel n = 8*(r>>2) + 4*(lane>>5) + (r&3),
+    // column = pixel m = lane & 31.  Registers 4q..4q+3 are 4 consecutive channels of one pixel:
+    // bias / ReLU / mask / accumulate / store run on float4 (16 B per lane).
     const bool relu = p.flags & PU_EPI_RELU;
     const bool accum = p.flags & PU_EPI_ACCUM;
     const bool shuffle = p.flags & PU_EPI_SHUFFLE2;
+    const bool vec = p.vec_epi;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-        const int n = n_blk + wn * (BN / WN) + j * 32 + lr;
-        if (n >= p.N) continue;
-        float* dst;
-        const float* msk;
-        int ld, nc;
-        float bv = 0.f;
-        int sh_c = 0, sh_i = 0, sh_j = 0;
+    for (int i = 0; i < FM; ++i) {
+        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+        if (m >= p.M) continue;
+        long long pix = m;
         if (shuffle) {
-            int ij = fdiv(n, p.dCo);
-            sh_c = n - ij * (p.N >> 2);
-            sh_i = ij >> 1;
-            sh_j = ij & 1;
-            dst = p.dst0;
-            msk = p.mask0;
-            ld = p.N >> 2;
-            nc = sh_c;
-            if (p.bias) bv = p.bias[sh_c];
-        } else if (n < p.n0) {
-            dst = p.dst0; msk = p.mask0; ld = p.n0; nc = n;
-            if (p.bias) bv = p.bias[n];
-        } else {
-            dst = p.dst1; msk = p.mask1; ld = p.N - p.n0; nc = n - p.n0;
-            if (p.bias) bv = p.bias[n];
+            const int t2 = fdiv(m, p.dWo);
+            const int wo = m - t2 * p.Wo;
+            const int bb = fdiv(t2, p.dHo);
+            const int ho = t2 - bb * p.Ho;
+            pix = ((long long)bb * 2 * p.Ho + 2 * ho) * (2 * p.Wo) + 2 * wo;   // + (sh_i*2Wo + sh_j)
         }
 #pragma unroll
-        for (int i = 0; i < FM; ++i) {
+        for (int j = 0; j < FN; ++j) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m_blk + wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (m >= p.M) continue;
+            for (int q = 0; q < 4; ++q) {
+                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                if (n >= p.N) continue;
+                float* dst;
+                const float* msk;
                 long long off;
+                int nb;   // bias index of the first channel
                 if (shuffle) {
-                    int t2 = fdiv(m, p.dWo);
-                    int wo = m - t2 * p.Wo;
-                    int bb = fdiv(t2, p.dHo);
-                    int ho = t2 - bb * p.Ho;
-                    long long pix = ((long long)bb * 2 * p.Ho + 2 * ho + sh_i) * (2 * p.Wo) + 2 * wo + sh_j;
-                    off = pix * ld + nc;
+                    const int co = p.N >> 2;
+                    const int ij = fdiv(n, p.dCo);
+                    const int c = n - ij * co;
+                    off = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
+                    dst = p.dst0; msk = p.mask0; nb = c;
+                } else if (n < p.n0) {
+                    off = pix * p.n0 + n;
+                    dst = p.dst0; msk = p.mask0; nb = n;
                 } else {
-                    off = (long long)m * ld + nc;
+                    off = pix * (p.N - p.n0) + (n - p.n0);
+                    dst = p.dst1; msk = p.mask1; nb = n;
                 }
-                float v = acc[i][j][r] + bv;
-                if (relu) v = fmaxf(v, 0.f);
-                if (msk && !(msk[off] > 0.f)) v = 0.f;
-                if (accum) v += dst[off];
-                dst[off] = v;
+                if (vec) {
+                    f32x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                    if (p.bias) {
+                        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + nb);
+                        v += bv;
+                    }
+                    if (relu) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                    }
+                    if (msk) {
+                        const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
+                    }
+                    if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
+                    *reinterpret_cast<f32x4*>(dst + off) = v;
+                } else {
+                    // odd channel counts: per element (channel n+e may cross the n0 split)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int ne = n + e;
+                        if (ne >= p.N) break;
+                        float* d;
+                        const float* mk;
+                        long long o;
+                        int bi = ne;
+                        if (shuffle) {
+                            const int co = p.N >> 2;
+                            const int ij = fdiv(ne, p.dCo);
+                            const int c = ne - ij * co;
+                            o = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
+                            d = p.dst0; mk = p.mask0; bi = c;
+                        } else if (ne < p.n0) {
+                            o = pix * p.n0 + ne; d = p.dst0; mk = p.mask0;
+                        } else {
+                            o = pix * (p.N - p.n0) + (ne - p.n0); d = p.dst1; mk = p.mask1;
+                        }
+                        float v = acc[i][j][4 * q + e] + (p.bias ? p.bias[bi] : 0.f);
+                        if (relu) v = fmaxf(v, 0.f);
+                        if (mk && !(mk[o] > 0.f)) v = 0.f;
+                        if (accum) v += d[o];
+                        d[o] = v;
+                    }
+                }
             }
         }
     }
@@ -317,6 +389,7 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     PU_REQUIRE(a->batch > 0 && a->in_h > 0 && a->in_w > 0 && a->out_h > 0 && a->out_w > 0,
                "pu_conv_igemm: bad grid %dx%dx%d -> %dx%d", a->batch, a->in_h, a->in_w, a->out_h, a->out_w);
     PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0, "pu_conv_igemm: bad taps");
+    PU_REQUIRE(a->kh * a->kw <= 32, "pu_conv_igemm: at most 32 taps");
     PU_REQUIRE(a->src0 && a->c0 > 0, "pu_conv_igemm: src0 missing");
     PU_REQUIRE(a->c1 == 0 || a->src1, "pu_conv_igemm: src1 missing for c1=%d", a->c1);
     PU_REQUIRE(a->weight && a->dst0 && a->n > 0, "pu_conv_igemm: weight/dst0/n");
@@ -336,15 +409,26 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     IgemmParams p;
     p.M = (int)M; p.N = a->n; p.K = K; p.k_pad = a->k_pad;
     p.Hi = a->in_h; p.Wi = a->in_w; p.Ho = a->out_h; p.Wo = a->out_w;
-    p.kw = a->kw; p.stride = a->stride; p.pad = a->pad;
+    p.kh = a->kh; p.kw = a->kw; p.stride = a->stride; p.pad = a->pad;
     p.C = C; p.c0 = a->c0; p.c1 = a->c1;
     p.src0 = a->src0; p.src1 = a->src1; p.wt = a->weight; p.bias = a->bias;
     p.dst0 = a->dst0; p.dst1 = a->dst1; p.mask0 = a->mask0; p.mask1 = a->mask1;
     p.n0 = shuffle ? a->n : a->n0; p.flags = a->flags;
     p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
     p.dC = make_fastdiv(C); p.dKw = make_fastdiv(a->kw); p.dCo = make_fastdiv(shuffle ? a->n / 4 : 1);
+    p.taps = a->kh * a->kw;
+    p.dTaps = make_fastdiv(p.taps);
+    p.cgroup = a->cgroup;
+    {
+        const uintptr_t al = (uintptr_t)a->dst0 | (uintptr_t)a->dst1 | (uintptr_t)a->mask0 | (uintptr_t)a->mask1 |
+                             (uintptr_t)a->bias;
+        p.vec_epi = (a->n % 4 == 0) && (p.n0 % 4 == 0) && (al & 15) == 0;
+    }
 
     const int mode = choose_mode(a->c0, a->c1);
+    PU_REQUIRE(a->cgroup == 0 || a->cgroup == 16 || a->cgroup == 32, "pu_conv_igemm: cgroup %d", a->cgroup);
+    PU_REQUIRE(a->cgroup == 0 || (mode == LOAD_CHUNK16 && a->c0 % a->cgroup == 0 && a->c1 % a->cgroup == 0),
+               "pu_conv_igemm: cgroup %d needs channel counts (%d, %d) that are multiples of it", a->cgroup, a->c0, a->c1);
     if (mode != LOAD_SCALAR) {
         PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0,
                    "pu_conv_igemm: sources must be 16-byte aligned");
@@ -355,7 +439,8 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     const int N = a->n;
     int bm, bn;
     choose_tile(M, N, &bm, &bn);
-    const dim3 grid(ceil_div(M, bm), ceil_div(N, bn));
+    p.gn = ceil_div(N, bn);
+    const dim3 grid(ceil_div(M, bm) * p.gn);
     if (bm == 256) launch_mode<256, 64, 4, 1>(mode, p, grid, s);
     else if (bm == 128 && bn == 128) launch_mode<128, 128, 2, 2>(mode, p, grid, s);
     else if (bm == 128) launch_mode<128, 64, 2, 2>(mode, p, grid, s);

@@ -29,6 +29,7 @@ struct WgradParams {
     int bias_mode;
     float* slab;
     int mps;  // pixel rows per split (multiple of WG_BM)
+    int gx, gy;  // k-tiles, n-tiles
     FastDiv dWo, dHo, dC, dKw;
 };
 
@@ -48,12 +49,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
     float* Qs = lds + 2 * WG_BM * BN;
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform -> scalar math
     const int wn = wave % WN, wk = wave / WN;
     const int lr = lane & 31, lh = lane >> 5;
-    const int n_blk = blockIdx.y * BN;
-    const int k_blk = blockIdx.x * BK;
-    const int m_begin = blockIdx.z * p.mps;
+    // XCD-aware order: logical tile = (split z, n-tile y, k-tile x), x fastest; each XCD walks a
+    // contiguous range, so the k-tiles that re-read the same pixel rows share its L2
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % p.gx;
+    const int tyz = tile / p.gx;
+    const int ty = tyz % p.gy;
+    const int tz = tyz / p.gy;
+    const int n_blk = ty * BN;
+    const int k_blk = tx * BK;
+    const int m_begin = tz * p.mps;
     const int m_end = min(p.M, m_begin + p.mps);
 
     // ---- fixed per-thread P columns
@@ -94,15 +103,25 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
             }
             rp[i] = v;
         }
+        // Q rows: the wave's first row is uniform (decomposed on the scalar unit); lanes add a
+        // small row delta (0 .. 64/Q_PER_ROW - 1) with carry into ho / b.
+        constexpr int QR_PER_WAVE = 64 / Q_PER_ROW;
+        const int q_delta = lane / Q_PER_ROW;
 #pragma unroll
         for (int i = 0; i < Q_LD; ++i) {
-            int m = m0 + q_row + i * (256 / Q_PER_ROW);
+            const int mu = m0 + wave * QR_PER_WAVE + i * (256 / Q_PER_ROW);
+            const int tu = fdiv(mu, p.dWo);
+            const int wou = mu - tu * p.Wo;
+            const int bu = fdiv(tu, p.dHo);
+            const int hou = tu - bu * p.Ho;
+            const int m = mu + q_delta;
+            int wo = wou + q_delta, ho = hou, b = bu;
+            while (wo >= p.Wo) {
+                wo -= p.Wo;
+                if (++ho >= p.Ho) { ho = 0; ++b; }
+            }
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if (m < m_end) {
-                int t = fdiv(m, p.dWo);
-                int wo = m - t * p.Wo;
-                int b = fdiv(t, p.dHo);
-                int ho = t - b * p.Ho;
                 long long pb = (long long)b * p.Hi * p.Wi;
                 int hb = ho * p.stride - p.pad, wb = wo * p.stride - p.pad;
                 if (QVEC) {
@@ -189,7 +208,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
     }
 
     // ---- partial tile -> slab[z][n][k]
-    float* slab = p.slab + (long long)blockIdx.z * p.Nr * p.Kc;
+    float* slab = p.slab + (long long)tz * p.Nr * p.Kc;
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
 #pragma unroll
@@ -338,7 +357,9 @@ extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes
     p.dC = make_fastdiv(pl.C); p.dKw = make_fastdiv(a->kw);
 
     hipStream_t s = as_stream(stream);
-    dim3 grid(ceil_div(pl.Kc, pl.BK), ceil_div(pl.Nr, pl.BN), pl.splits);
+    p.gx = ceil_div(pl.Kc, pl.BK);
+    p.gy = ceil_div(pl.Nr, pl.BN);
+    dim3 grid(p.gx * p.gy * pl.splits);
 #define PU_WG_LAUNCH(BN_, BK_, WN_, WK_)                                                              \
     do {                                                                                               \
         if (pl.qvec) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, true>), grid, dim3(256), 0, s, p);  \

@@ -1,0 +1,63 @@
+"""Forward-only validation - drop-in for yaricom/Plastic-UNet src/eval.py (eval_net, :66-103).
+
+The reference evaluates one sample at a time with a ZERO trace whose update is discarded (S5), a
+BCE loss and fast_iou_metric on the host.  Here the samples go through the HIP forward in chunks
+of ``batch`` slots (each slot with a zero trace - identical per-sample math), and the per-sample
+loss / metric averages are the reference's.
+"""
+from optparse import OptionParser
+
+import numpy as np
+import torch
+
+from punet import bce_loss
+from utils import fast_iou_metric
+
+
+def _device_of(net):
+    return next(net.parameters()).device
+
+
+def eval_net(net, X_val, y_val, device, criterion=None, debug=False, batch=32):
+    """Returns (accuracy, loss) averaged over samples, as eval.py:66-103."""
+    net.eval()
+    n = len(X_val)
+    total_acc, total_loss = 0.0, 0.0
+    with torch.no_grad():
+        for s in range(0, n, batch):
+            xb = torch.from_numpy(np.asarray(X_val[s:s + batch], dtype=np.float32)).to(device)
+            tb = torch.from_numpy(np.asarray(y_val[s:s + batch], dtype=np.float32)).to(device)
+            B = xb.shape[0]
+            hebb = net.initialZeroHebb(B)          # zero trace per slot; the update is discarded
+            y, _ = net(xb, hebb)
+            for b in range(B):
+                yf = y[b].reshape(-1)
+                tf = tb[b].reshape(-1)
+                loss = criterion(yf, tf) if criterion is not None else bce_loss(yf, tf)
+                total_loss += loss.item()
+                total_acc += fast_iou_metric(y_true_in=tf.cpu().numpy(), y_pred_in=yf.cpu().numpy())
+    return total_acc / n, total_loss / n
+
+
+def get_args():
+    parser = OptionParser()
+    parser.add_option('--model', '-m', default='MODEL.pth', help="the file with the model state_dict")
+    parser.add_option('-i', '--data', dest='data_dir', type='string', help='dataset .npz (x_valid, y_valid)')
+    parser.add_option('-g', '--gpu', action='store_true', dest='gpu', default=True, help='use the GPU (always)')
+    parser.add_option('-v', '--debug', action='store_true', dest='debug', default=False)
+    parser.add_option('--model-type', dest='model_type', default='unetpres', help='unetpres | unetp')
+    parser.add_option('--nbf', dest='nbf', type='int', default=101)
+    (options, args) = parser.parse_args()
+    return options
+
+
+if __name__ == "__main__":
+    args = get_args()
+    device = torch.device('cuda')
+    from unet import UNetp, UNetpRes
+    cls = UNetpRes if args.model_type == 'unetpres' else UNetp
+    net = cls(n_channels=1, n_classes=1, device=device, nbf=args.nbf)
+    net.load_state_dict(torch.load(args.model, weights_only=True))
+    d = np.load(args.data_dir)
+    acc, loss = eval_net(net, d["x_valid"], d["y_valid"], device)
+    print("Validation accuracy: %f, loss: %f" % (acc, loss))

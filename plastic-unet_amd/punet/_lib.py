@@ -26,7 +26,7 @@ class ConvArgs(ctypes.Structure):
     _fields_ = [("batch", c_int), ("in_h", c_int), ("in_w", c_int), ("out_h", c_int), ("out_w", c_int),
                 ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int),
                 ("src0", P), ("c0", c_int), ("src1", P), ("c1", c_int),
-                ("weight", P), ("k_pad", c_int), ("n", c_int), ("bias", P),
+                ("weight", P), ("k_pad", c_int), ("cgroup", c_int), ("n", c_int), ("bias", P),
                 ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int)]
 
 
@@ -63,7 +63,7 @@ SIGNATURES = [
     ("pu_wgrad", c_int, [ctypes.POINTER(WgradArgs), P, c_size, P]),
     ("pu_wgrad_tile", c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
-    ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_nchw_to_nhwc", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_maxpool2_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_maxpool2_bwd", c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),

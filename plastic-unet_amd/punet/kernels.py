@@ -13,7 +13,7 @@ from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticBwdArgs, AdamTensor,
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
-           "bce_bwd", "adam_multi", "round16", "device_info", "lib"]
+           "bce_bwd", "adam_multi", "round16", "cgroup_for", "device_info", "lib"]
 
 
 def lib():
@@ -106,16 +106,25 @@ def device_info(device=0):
     return cu.value, clk.value, mem.value
 
 
+def cgroup_for(c0, c1=0):
+    """K order for a packed conv operand: 32-channel groups when both sources allow it."""
+    if c0 % 32 == 0 and c1 % 32 == 0:
+        return 32
+    if c0 % 16 == 0 and c1 % 16 == 0:
+        return 16
+    return 0
+
+
 def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, dst0, n0=None,
           src1=None, c1=0, bias=None, dst1=None, mask0=None, mask1=None, relu=False, accum=False,
-          shuffle=False):
+          shuffle=False, cgroup=0):
     """pu_conv_igemm: implicit-GEMM conv (3x3 fwd/dgrad, ConvT fwd with shuffle, ConvT dgrad)."""
     for t, nm in ((src0, "src0"), (src1, "src1"), (weight, "weight"), (bias, "bias"), (dst0, "dst0"),
                   (dst1, "dst1"), (mask0, "mask0"), (mask1, "mask1")):
         _req(t, nm)
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
-                 _p(src0), c0, _p(src1), c1, _p(weight), k_pad, n, _p(bias),
+                 _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags)
     if _PROF is None:
         check(lib().pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
@@ -152,7 +161,7 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
         check(L.pu_wgrad(ctypes.byref(a), ws.data_ptr(), nbytes, _stream()), "pu_wgrad")
 
 
-def pack_weight(w, mode, k_pad, out=None):
+def pack_weight(w, mode, k_pad, out=None, cgroup=0):
     _req(w, "w")
     d0, d1, kh, kw = w.shape
     taps = kh * kw
@@ -160,7 +169,7 @@ def pack_weight(w, mode, k_pad, out=None):
     if out is None:
         out = torch.empty(rows, k_pad, dtype=torch.float32, device=w.device)
     with _Rec("pack_weight", nbytes=4.0 * (w.numel() + out.numel())):
-        check(lib().pu_pack_weight(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, _stream()),
+        check(lib().pu_pack_weight(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, cgroup, _stream()),
               "pu_pack_weight")
     return out
 

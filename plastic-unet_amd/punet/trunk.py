@@ -27,14 +27,14 @@ class _Packs:
     def __init__(self):
         self.cache = {}
 
-    def get(self, w, mode, k_pad):
+    def get(self, w, mode, k_pad, cgroup=0):
         # keyed by storage (detached views share the parameter's version counter)
-        key = (w.data_ptr(), tuple(w.shape), mode)
+        key = (w.data_ptr(), tuple(w.shape), mode, cgroup)
         ver = w._version
         hit = self.cache.get(key)
         if hit is not None and hit[0] == ver:
             return hit[1]
-        packed = K.pack_weight(w.detach(), mode, k_pad)
+        packed = K.pack_weight(w.detach(), mode, k_pad, cgroup=cgroup)
         self.cache[key] = (ver, packed)
         return packed
 
@@ -45,9 +45,11 @@ def conv3x3(x0, w, b, packs, x1=None, relu=True):
     c1 = 0 if x1 is None else x1.shape[3]
     cout = w.shape[0]
     k_pad = K.round16(9 * (c0 + c1))
+    g = K.cgroup_for(c0, c1)
     out = torch.empty(B, H, W, cout, dtype=torch.float32, device=x0.device)
     K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=x0, c0=c0, src1=x1, c1=c1,
-            weight=packs.get(w, PU_PACK_CONV_FWD, k_pad), k_pad=k_pad, n=cout, bias=b, dst0=out, relu=relu)
+            weight=packs.get(w, PU_PACK_CONV_FWD, k_pad, g), k_pad=k_pad, n=cout, bias=b, dst0=out, relu=relu,
+            cgroup=g)
     return out
 
 
@@ -56,12 +58,13 @@ def conv3x3_dgrad(dz, w, packs, split=None, mask0=None, mask1=None):
     B, H, W, cout = dz.shape
     cin = w.shape[1]
     k_pad = K.round16(9 * cout)
+    g = K.cgroup_for(cout)
     n0 = cin if split is None else split
     d0 = torch.empty(B, H, W, n0, dtype=torch.float32, device=dz.device)
     d1 = None if split is None else torch.empty(B, H, W, cin - n0, dtype=torch.float32, device=dz.device)
     K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=dz, c0=cout,
-            weight=packs.get(w, PU_PACK_CONV_DGRAD, k_pad), k_pad=k_pad, n=cin, dst0=d0, n0=n0, dst1=d1,
-            mask0=mask0, mask1=mask1)
+            weight=packs.get(w, PU_PACK_CONV_DGRAD, k_pad, g), k_pad=k_pad, n=cin, dst0=d0, n0=n0, dst1=d1,
+            mask0=mask0, mask1=mask1, cgroup=g)
     return d0, d1
 
 
@@ -96,9 +99,10 @@ def convT2x2_dgrad(du, w, packs, mask):
     B, H2, W2, cout = du.shape
     cin = w.shape[0]
     k_pad = K.round16(4 * cout)
+    g = K.cgroup_for(cout)
     dx = torch.empty(B, H2 // 2, W2 // 2, cin, dtype=torch.float32, device=du.device)
     K.igemm(batch=B, in_hw=(H2, W2), out_hw=(H2 // 2, W2 // 2), k=2, stride=2, pad=0, src0=du, c0=cout,
-            weight=packs.get(w, PU_PACK_CONVT_DGRAD, k_pad), k_pad=k_pad, n=cin, dst0=dx, mask0=mask)
+            weight=packs.get(w, PU_PACK_CONVT_DGRAD, k_pad, g), k_pad=k_pad, n=cin, dst0=dx, mask0=mask, cgroup=g)
     return dx
 
 
