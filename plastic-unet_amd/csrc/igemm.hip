@@ -19,6 +19,10 @@
 #ifndef PU_ABLATE
 #define PU_ABLATE 0
 #endif
+// 1: use only the register-staged kernel (A/B against the direct-to-LDS one)
+#ifndef PU_NO_DMA
+#define PU_NO_DMA 0
+#endif
 
 namespace pu {
 
@@ -83,6 +87,105 @@ __device__ __forceinline__ f32x4 load_a4(const IgemmParams& p, int pb, int hb, i
             }
         }
         return v;
+    }
+}
+
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m_blk,
+                                         int n_blk, int wm, int wn, int lr, int lh) {
+    constexpr int FM = BM / WM / 32;
+    constexpr int FN = BN / WN / 32;
+    // ---- epilogue.  acc[i][j] = D^T block: MFMA row = channel n = 8*(r>>2) + 4*(lane>>5) + (r&3),
+    // column = pixel m = lane & 31.  Registers 4q..4q+3 are 4 consecutive channels of one pixel:
+    // bias / ReLU / mask / accumulate / store run on float4 (16 B per lane).
+    const bool relu = p.flags & PU_EPI_RELU;
+    const bool accum = p.flags & PU_EPI_ACCUM;
+    const bool shuffle = p.flags & PU_EPI_SHUFFLE2;
+    const bool vec = p.vec_epi;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+        if (m >= p.M) continue;
+        long long pix = m;
+        if (shuffle) {
+            const int t2 = fdiv(m, p.dWo);
+            const int wo = m - t2 * p.Wo;
+            const int bb = fdiv(t2, p.dHo);
+            const int ho = t2 - bb * p.Ho;
+            pix = ((long long)bb * 2 * p.Ho + 2 * ho) * (2 * p.Wo) + 2 * wo;   // + (sh_i*2Wo + sh_j)
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                if (n >= p.N) continue;
+                float* dst;
+                const float* msk;
+                long long off;
+                int nb;   // bias index of the first channel
+                if (shuffle) {
+                    const int co = p.N >> 2;
+                    const int ij = fdiv(n, p.dCo);
+                    const int c = n - ij * co;
+                    off = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
+                    dst = p.dst0; msk = p.mask0; nb = c;
+                } else if (n < p.n0) {
+                    off = pix * p.n0 + n;
+                    dst = p.dst0; msk = p.mask0; nb = n;
+                } else {
+                    off = pix * (p.N - p.n0) + (n - p.n0);
+                    dst = p.dst1; msk = p.mask1; nb = n;
+                }
+                if (vec) {
+                    f32x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                    if (p.bias) {
+                        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + nb);
+                        v += bv;
+                    }
+                    if (relu) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                    }
+                    if (msk) {
+                        const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
+                    }
+                    if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
+                    *reinterpret_cast<f32x4*>(dst + off) = v;
+                } else {
+                    // odd channel counts: per element (channel n+e may cross the n0 split)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int ne = n + e;
+                        if (ne >= p.N) break;
+                        float* d;
+                        const float* mk;
+                        long long o;
+                        int bi = ne;
+                        if (shuffle) {
+                            const int co = p.N >> 2;
+                            const int ij = fdiv(ne, p.dCo);
+                            const int c = ne - ij * co;
+                            o = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
+                            d = p.dst0; mk = p.mask0; bi = c;
+                        } else if (ne < p.n0) {
+                            o = pix * p.n0 + ne; d = p.dst0; mk = p.mask0;
+                        } else {
+                            o = pix * (p.N - p.n0) + (ne - p.n0); d = p.dst1; mk = p.mask1;
+                        }
+                        float v = acc[i][j][4 * q + e] + (p.bias ? p.bias[bi] : 0.f);
+                        if (relu) v = fmaxf(v, 0.f);
+                        if (mk && !(mk[o] > 0.f)) v = 0.f;
+                        if (accum) v += d[o];
+                        d[o] = v;
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -250,98 +353,161 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
         if (PU_ABLATE != 4) __syncthreads();
     }
 
-    // ---- epilogue.  acc[i][j] = D^T block: MFMA row = channel n = 8*(r>>2) + 4*(lane>>5) + (r&3),
-    // column = pixel m = lane & 31.  Registers 4q..4q+3 are 4 consecutive channels of one pixel:
-    // bias / ReLU / mask / accumulate / store run on float4 (16 B per lane).
-    const bool relu = p.flags & PU_EPI_RELU;
-    const bool accum = p.flags & PU_EPI_ACCUM;
-    const bool shuffle = p.flags & PU_EPI_SHUFFLE2;
-    const bool vec = p.vec_epi;
+    epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
+}
+
+// ------------------------------------------------------------------------ direct-to-LDS variant
+// For 16-channel-chunk loads (every conv with C % 16 == 0 - all but the 1-channel stem) the A and
+// B tiles are fetched with global_load_lds_dwordx4: no VGPR staging, no ds_write, loads stay in
+// flight across the barrier.  LDS image per stage: rows of 64 B (16 floats), unpadded; the
+// 16-byte chunk kc of row r is stored at position kc ^ ((r >> 2) & 3) (XOR swizzle on the global
+// SOURCE address, same XOR on the ds_read_b128 address) so the MFMA operand reads are
+// conflict-free.  NBUF-deep ring with a counted s_waitcnt vmcnt and a raw s_barrier per stage.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+__device__ __attribute__((aligned(16))) float g_zero16[4];
+
+template <int BM, int BN, int WM, int WN, int NBUF>
+__global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
+    constexpr int FM = BM / WM / 32;
+    constexpr int FN = BN / WN / 32;
+    constexpr int A_LD = BM / 64;   // glds per wave per stage (16 rows x 64 B each)
+    constexpr int B_LD = BN / 64;
+    constexpr int G = A_LD + B_LD;
+    constexpr int STAGE = (BM + BN) * 16;   // floats per ring slot
+    static_assert(WM * WN == 4, "4 waves");
+
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mb = tile / p.gn;
+    const int m_blk = mb * BM;
+    const int n_blk = (tile - mb * p.gn) * BN;
+
+    // loader: instruction j of this wave covers tile rows wave*(BM/4) + 16j + (lane >> 2);
+    // lane stores LDS position (lane & 3) of its row, i.e. logical chunk kc (the swizzle only
+    // depends on lane bits because the row bases are multiples of 16)
+    const int lq = lane >> 2;
+    const int kc = (lane & 3) ^ ((lane >> 4) & 3);
+    long long rb0[A_LD], rb1[A_LD];
+    unsigned tmask[A_LD];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
-        if (m >= p.M) continue;
-        long long pix = m;
-        if (shuffle) {
-            const int t2 = fdiv(m, p.dWo);
-            const int wo = m - t2 * p.Wo;
-            const int bb = fdiv(t2, p.dHo);
-            const int ho = t2 - bb * p.Ho;
-            pix = ((long long)bb * 2 * p.Ho + 2 * ho) * (2 * p.Wo) + 2 * wo;   // + (sh_i*2Wo + sh_j)
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
-                if (n >= p.N) continue;
-                float* dst;
-                const float* msk;
-                long long off;
-                int nb;   // bias index of the first channel
-                if (shuffle) {
-                    const int co = p.N >> 2;
-                    const int ij = fdiv(n, p.dCo);
-                    const int c = n - ij * co;
-                    off = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
-                    dst = p.dst0; msk = p.mask0; nb = c;
-                } else if (n < p.n0) {
-                    off = pix * p.n0 + n;
-                    dst = p.dst0; msk = p.mask0; nb = n;
-                } else {
-                    off = pix * (p.N - p.n0) + (n - p.n0);
-                    dst = p.dst1; msk = p.mask1; nb = n;
-                }
-                if (vec) {
-                    f32x4 v;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-                    if (p.bias) {
-                        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + nb);
-                        v += bv;
-                    }
-                    if (relu) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-                    }
-                    if (msk) {
-                        const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
-                    }
-                    if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
-                    *reinterpret_cast<f32x4*>(dst + off) = v;
-                } else {
-                    // odd channel counts: per element (channel n+e may cross the n0 split)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int ne = n + e;
-                        if (ne >= p.N) break;
-                        float* d;
-                        const float* mk;
-                        long long o;
-                        int bi = ne;
-                        if (shuffle) {
-                            const int co = p.N >> 2;
-                            const int ij = fdiv(ne, p.dCo);
-                            const int c = ne - ij * co;
-                            o = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
-                            d = p.dst0; mk = p.mask0; bi = c;
-                        } else if (ne < p.n0) {
-                            o = pix * p.n0 + ne; d = p.dst0; mk = p.mask0;
-                        } else {
-                            o = pix * (p.N - p.n0) + (ne - p.n0); d = p.dst1; mk = p.mask1;
-                        }
-                        float v = acc[i][j][4 * q + e] + (p.bias ? p.bias[bi] : 0.f);
-                        if (relu) v = fmaxf(v, 0.f);
-                        if (mk && !(mk[o] > 0.f)) v = 0.f;
-                        if (accum) v += d[o];
-                        d[o] = v;
-                    }
-                }
-            }
+    for (int j = 0; j < A_LD; ++j) {
+        const int m = m_blk + wave * (BM / 4) + 16 * j + lq;
+        rb0[j] = 0; rb1[j] = 0; tmask[j] = 0;
+        if (m < p.M) {
+            const int t = fdiv(m, p.dWo);
+            const int wo = m - t * p.Wo;
+            const int b = fdiv(t, p.dHo);
+            const int ho = t - b * p.Ho;
+            const int hb = ho * p.stride - p.pad, wb = wo * p.stride - p.pad;
+            const long long pix0 = (long long)b * p.Hi * p.Wi + (long long)hb * p.Wi + wb;
+            rb0[j] = pix0 * p.c0 + kc * 4;
+            rb1[j] = pix0 * p.c1 + kc * 4;
+            unsigned msk = 0;
+            for (int r = 0; r < p.kh; ++r)
+                for (int q = 0; q < p.kw; ++q)
+                    if ((unsigned)(hb + r) < (unsigned)p.Hi && (unsigned)(wb + q) < (unsigned)p.Wi)
+                        msk |= 1u << (r * p.kw + q);
+            tmask[j] = msk;
         }
     }
+    const float* wrow[B_LD];
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+        const int n = n_blk + wave * (BN / 4) + 16 * j + lq;
+        wrow[j] = n < p.N ? p.wt + (long long)n * p.k_pad + kc * 4 : nullptr;
+    }
+
+    const int T = p.k_pad / IG_BK;
+    auto issue = [&](int t, int slot) {
+        const int k0 = t * IG_BK;
+        int tap, c;
+        if (p.cgroup) {
+            const int per = p.cgroup >> 4;
+            const int tg = per == 2 ? (t >> 1) : t;
+            const int h = per == 2 ? (t & 1) : 0;
+            const int g = fdiv(tg, p.dTaps);
+            tap = tg - g * p.taps;
+            c = g * p.cgroup + h * 16;
+        } else {
+            tap = fdiv(k0, p.dC);
+            c = k0 - tap * p.C;
+        }
+        const int r = fdiv(tap, p.dKw);
+        const int s = tap - r * p.kw;
+        const bool first = c < p.c0;
+        const float* src = first ? p.src0 : p.src1;
+        const int cs = first ? p.c0 : p.c1;
+        const long long off = (long long)(r * p.Wi + s) * cs + (first ? c : c - p.c0);
+        const unsigned bit = (k0 < p.K) ? (1u << tap) : 0u;
+        float* a_slot = lds + slot * STAGE;
+        float* b_slot = a_slot + BM * 16;
+#pragma unroll
+        for (int j = 0; j < A_LD; ++j) {
+            const float* g = (tmask[j] & bit) ? src + (first ? rb0[j] : rb1[j]) + off : g_zero16;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(a_slot + (wave * (BM / 4) + 16 * j) * 16),
+                                             16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < B_LD; ++j) {
+            const float* g = wrow[j] ? wrow[j] + k0 : g_zero16;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(b_slot + (wave * (BN / 4) + 16 * j) * 16),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int a_row0 = wm * (BM / WM) + lr;
+    const int b_row0 = wn * (BN / WN) + lr;
+    const int swz = (lr >> 2) & 3;   // ((row >> 2) & 3) of every row this lane reads
+
+#pragma unroll
+    for (int s0 = 0; s0 < NBUF - 1; ++s0)
+        if (s0 < T) issue(s0, s0);
+
+    for (int t = 0; t < T; ++t) {
+        // stage t has landed (own loads) when at most the younger stages' G loads are pending
+        if (t + NBUF - 2 < T) {
+            if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();   // everyone's stage-t loads landed; slot (t-1) is free
+        if (t + NBUF - 1 < T) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
+        const float* a = lds + (t % NBUF) * STAGE;
+        const float* b = a + BM * 16;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int pos = ((kk * 2 + lh) ^ swz) * 4;
+            f32x4 fa[FM], fb[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const f32x4*>(b + (b_row0 + j * 32) * 16 + pos);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
+        }
+    }
+    epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
 }
 
 // ------------------------------------------------------------------------------------------ host
@@ -441,7 +607,12 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     choose_tile(M, N, &bm, &bn);
     p.gn = ceil_div(N, bn);
     const dim3 grid(ceil_div(M, bm) * p.gn);
-    if (bm == 256) launch_mode<256, 64, 4, 1>(mode, p, grid, s);
+    if (mode == LOAD_CHUNK16 && !PU_NO_DMA) {
+        if (bm == 256) hipLaunchKernelGGL((igemm_dma_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
+        else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 128, 2, 2, 3>), grid, dim3(256), 0, s, p);
+        else if (bm == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((igemm_dma_kernel<64, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
+    } else if (bm == 256) launch_mode<256, 64, 4, 1>(mode, p, grid, s);
     else if (bm == 128 && bn == 128) launch_mode<128, 128, 2, 2>(mode, p, grid, s);
     else if (bm == 128) launch_mode<128, 64, 2, 2>(mode, p, grid, s);
     else launch_mode<64, 64, 2, 2>(mode, p, grid, s);
