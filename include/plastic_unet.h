@@ -74,6 +74,10 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
  *   ACCUM: dst += v else dst = v.  Columns [0,n0) go to dst0 (NHWC, n0 channels), [n0,n) to
  *   dst1 (NHWC, n-n0 channels).  SHUFFLE2: n = (2i+j)*co + c is stored at pixel (2ho+i, 2wo+j)
  *   of a (2*out_h, 2*out_w) NHWC grid with co = n/4 channels and bias[c] (ConvTranspose2d 2x2 s2).
+ * workspace (optional): when the M x N tile grid cannot fill the chip (small pixel grids: the
+ *   8x8 / 16x16 levels of the U-Net) and ws_bytes >= pu_conv_igemm_workspace_bytes(a), K is split
+ *   over ksplit blocks per tile; the partial tiles go to the workspace and a second kernel sums
+ *   them in fixed split order (deterministic) and runs the epilogue above.  NULL -> no split.
  * ------------------------------------------------------------------------------------------- */
 enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4 };
 
@@ -92,12 +96,16 @@ typedef struct {
     const float* mask0;
     const float* mask1;
     int flags;
+    void* workspace; size_t ws_bytes;
 } pu_conv_args;
 
 int pu_conv_igemm(const pu_conv_args* a, void* stream);
-/* the kernel instantiation pu_conv_igemm would launch: block tile bm x bn and A-loader mode
- * (0 = 16-channel chunks, 1 = float4, 2 = scalar); for profiling/roofline attribution */
-int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* mode);
+/* split-K scratch pu_conv_igemm would use for these arguments (0: no split planned) */
+size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a);
+/* the kernel instantiation pu_conv_igemm would launch: block tile bm x bn, A-loader mode
+ * (0 = 16-channel chunks, 1 = float4, 2 = scalar) and K splits (1 = none; counts a->workspace);
+ * for profiling/roofline attribution */
+int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* mode, int* ksplit);
 
 /* ---------------------------------------------------------------------------------------------
  * Weight/bias gradient of a convolution as a split-K MFMA GEMM over the B*H*W pixel rows:

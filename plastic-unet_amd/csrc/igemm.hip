@@ -49,6 +49,8 @@ struct IgemmParams {
     int n0, flags;
     int cgroup, taps, gn;   // K order (0 tap-major, 16/32 channel-group-major), kh*kw, n-blocks
     int vec_epi;            // float4 epilogue (channel counts % 4 == 0, 16-byte aligned buffers)
+    int ksplit, t_per;      // split-K: blocks per tile and 16-wide K stages per split
+    float* part;            // split-K partial tiles [ksplit][M][N]
     FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
 };
 
@@ -90,6 +92,49 @@ __device__ __forceinline__ f32x4 load_a4(const IgemmParams& p, int pb, int hb, i
     }
 }
 
+// Output pixel base of GEMM row m (SHUFFLE2: the top-left pixel of its 2x2 output block).
+__device__ __forceinline__ long long epi_pix(const IgemmParams& p, int m) {
+    if (!(p.flags & PU_EPI_SHUFFLE2)) return m;
+    const int t2 = fdiv(m, p.dWo);
+    const int wo = m - t2 * p.Wo;
+    const int bb = fdiv(t2, p.dHo);
+    const int ho = t2 - bb * p.Ho;
+    return ((long long)bb * 2 * p.Ho + 2 * ho) * (2 * p.Wo) + 2 * wo;
+}
+
+// float4 epilogue of channels n..n+3 (n % 4 == 0, vec_epi) of the row with output pixel base pix.
+__device__ __forceinline__ void epi_store4(const IgemmParams& p, long long pix, int n, f32x4 v) {
+    float* dst;
+    const float* msk;
+    long long off;
+    int nb;   // bias index of the first channel
+    if (p.flags & PU_EPI_SHUFFLE2) {
+        const int co = p.N >> 2;
+        const int ij = fdiv(n, p.dCo);
+        const int c = n - ij * co;
+        off = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
+        dst = p.dst0; msk = p.mask0; nb = c;
+    } else if (n < p.n0) {
+        off = pix * p.n0 + n;
+        dst = p.dst0; msk = p.mask0; nb = n;
+    } else {
+        off = pix * (p.N - p.n0) + (n - p.n0);
+        dst = p.dst1; msk = p.mask1; nb = n;
+    }
+    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + nb);
+    if (p.flags & PU_EPI_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (msk) {
+        const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
+    }
+    if (p.flags & PU_EPI_ACCUM) v += *reinterpret_cast<const f32x4*>(dst + off);
+    *reinterpret_cast<f32x4*>(dst + off) = v;
+}
+
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m_blk,
                                          int n_blk, int wm, int wn, int lr, int lh) {
@@ -106,56 +151,18 @@ __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM 
     for (int i = 0; i < FM; ++i) {
         const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
         if (m >= p.M) continue;
-        long long pix = m;
-        if (shuffle) {
-            const int t2 = fdiv(m, p.dWo);
-            const int wo = m - t2 * p.Wo;
-            const int bb = fdiv(t2, p.dHo);
-            const int ho = t2 - bb * p.Ho;
-            pix = ((long long)bb * 2 * p.Ho + 2 * ho) * (2 * p.Wo) + 2 * wo;   // + (sh_i*2Wo + sh_j)
-        }
+        const long long pix = epi_pix(p, m);
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
                 if (n >= p.N) continue;
-                float* dst;
-                const float* msk;
-                long long off;
-                int nb;   // bias index of the first channel
-                if (shuffle) {
-                    const int co = p.N >> 2;
-                    const int ij = fdiv(n, p.dCo);
-                    const int c = n - ij * co;
-                    off = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
-                    dst = p.dst0; msk = p.mask0; nb = c;
-                } else if (n < p.n0) {
-                    off = pix * p.n0 + n;
-                    dst = p.dst0; msk = p.mask0; nb = n;
-                } else {
-                    off = pix * (p.N - p.n0) + (n - p.n0);
-                    dst = p.dst1; msk = p.mask1; nb = n;
-                }
                 if (vec) {
                     f32x4 v;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-                    if (p.bias) {
-                        const f32x4 bv = *reinterpret_cast<const f32x4*>(p.bias + nb);
-                        v += bv;
-                    }
-                    if (relu) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-                    }
-                    if (msk) {
-                        const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
-                    }
-                    if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
-                    *reinterpret_cast<f32x4*>(dst + off) = v;
+                    epi_store4(p, pix, n, v);
                 } else {
                     // odd channel counts: per element (channel n+e may cross the n0 split)
 #pragma unroll
@@ -384,7 +391,9 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave % WM, wn = wave / WM;
     const int lr = lane & 31, lh = lane >> 5;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kz = tile / (gridDim.x / p.ksplit);   // K split (outermost: a split's blocks share its weight slice)
+    tile -= kz * (gridDim.x / p.ksplit);
     const int mb = tile / p.gn;
     const int m_blk = mb * BM;
     const int n_blk = (tile - mb * p.gn) * BN;
@@ -424,8 +433,10 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
         wrow[j] = n < p.N ? p.wt + (long long)n * p.k_pad + kc * 4 : nullptr;
     }
 
-    const int T = p.k_pad / IG_BK;
-    auto issue = [&](int t, int slot) {
+    const int t0 = kz * p.t_per;
+    const int T = min(p.k_pad / IG_BK - t0, p.t_per);
+    auto issue = [&](int tl, int slot) {
+        const int t = t0 + tl;
         const int k0 = t * IG_BK;
         int tap, c;
         if (p.cgroup) {
@@ -507,7 +518,42 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
         }
     }
-    epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
+    if (p.ksplit == 1) {
+        epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
+        return;
+    }
+    // split-K: raw partial tile -> part[kz][m][n] (float4 over 4 consecutive n; N % 4 == 0)
+    float* part = p.part + (long long)kz * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                if (n >= p.N) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                *reinterpret_cast<f32x4*>(part + (long long)m * p.N + n) = v;
+            }
+    }
+}
+
+// split-K second pass: sum the partial tiles in split order (deterministic) + the fused epilogue
+__global__ __launch_bounds__(256) void igemm_splitk_epilogue_kernel(const IgemmParams p) {
+    const int nq = p.N >> 2;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)p.M * nq) return;
+    const int m = (int)(idx / nq);
+    const int n = (int)(idx - (long long)m * nq) * 4;
+    const long long mn = (long long)p.M * p.N;
+    const float* src = p.part + (long long)m * p.N + n;
+    f32x4 v = *reinterpret_cast<const f32x4*>(src);
+    for (int z = 1; z < p.ksplit; ++z) v += *reinterpret_cast<const f32x4*>(src + z * mn);
+    epi_store4(p, epi_pix(p, m), n, v);
 }
 
 // ------------------------------------------------------------------------------------------ host
@@ -544,6 +590,35 @@ static int choose_mode(int c0, int c1) {
     if (c0 % 16 == 0 && c1 % 16 == 0) return LOAD_CHUNK16;
     if (c0 % 4 == 0 && c1 % 4 == 0) return LOAD_VEC4;
     return LOAD_SCALAR;
+}
+
+static bool vec_epilogue(const pu_conv_args* a) {
+    const bool shuffle = a->flags & PU_EPI_SHUFFLE2;
+    const int n0 = shuffle ? a->n : a->n0;
+    const uintptr_t al = (uintptr_t)a->dst0 | (uintptr_t)a->dst1 | (uintptr_t)a->mask0 | (uintptr_t)a->mask1 |
+                         (uintptr_t)a->bias;
+    return (a->n % 4 == 0) && (n0 % 4 == 0) && (al & 15) == 0;
+}
+
+// Split-K plan: when the M x N tile grid fills fewer than the resident block slots of the chip
+// (256 CUs x blocks per CU of the tile), split the K stages so that it does, keeping >= 8 stages
+// (128 k) per split.  Only the direct-to-LDS kernel splits.
+static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* ksplit, int* t_per) {
+    const int T = a->k_pad / IG_BK;
+    *ksplit = 1;
+    *t_per = T;
+    if (PU_NO_DMA || choose_mode(a->c0, a->c1) != LOAD_CHUNK16 || !vec_epilogue(a)) return;
+    const int occ = (bm == 256) ? 2 : (bm == 128 && bn == 128) ? 3 : 4;   // LDS-limited (3-deep ring)
+    const int blocks = blocks_for(M, a->n, bm, bn);
+    int ks = (256 * occ) / blocks;
+    if (ks > T / 8) ks = T / 8;
+    if (ks < 2) return;
+    *t_per = ceil_div(T, ks);
+    *ksplit = ceil_div(T, *t_per);
+}
+
+static size_t split_bytes(long long M, int n, int ksplit) {
+    return ksplit > 1 ? (size_t)ksplit * (size_t)M * (size_t)n * sizeof(float) : 0;
 }
 
 }  // namespace pu
@@ -585,11 +660,7 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     p.taps = a->kh * a->kw;
     p.dTaps = make_fastdiv(p.taps);
     p.cgroup = a->cgroup;
-    {
-        const uintptr_t al = (uintptr_t)a->dst0 | (uintptr_t)a->dst1 | (uintptr_t)a->mask0 | (uintptr_t)a->mask1 |
-                             (uintptr_t)a->bias;
-        p.vec_epi = (a->n % 4 == 0) && (p.n0 % 4 == 0) && (al & 15) == 0;
-    }
+    p.vec_epi = vec_epilogue(a);
 
     const int mode = choose_mode(a->c0, a->c1);
     PU_REQUIRE(a->cgroup == 0 || a->cgroup == 16 || a->cgroup == 32, "pu_conv_igemm: cgroup %d", a->cgroup);
@@ -606,7 +677,13 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     int bm, bn;
     choose_tile(M, N, &bm, &bn);
     p.gn = ceil_div(N, bn);
-    const dim3 grid(ceil_div(M, bm) * p.gn);
+    plan_split(a, M, bm, bn, &p.ksplit, &p.t_per);
+    if (p.ksplit > 1 && (!a->workspace || a->ws_bytes < split_bytes(M, N, p.ksplit))) {
+        p.ksplit = 1;                       // no scratch: unsplit
+        p.t_per = a->k_pad / IG_BK;
+    }
+    p.part = (float*)a->workspace;
+    const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
     if (mode == LOAD_CHUNK16 && !PU_NO_DMA) {
         if (bm == 256) hipLaunchKernelGGL((igemm_dma_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
         else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 128, 2, 2, 3>), grid, dim3(256), 0, s, p);
@@ -616,13 +693,31 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     else if (bm == 128 && bn == 128) launch_mode<128, 128, 2, 2>(mode, p, grid, s);
     else if (bm == 128) launch_mode<128, 64, 2, 2>(mode, p, grid, s);
     else launch_mode<64, 64, 2, 2>(mode, p, grid, s);
+    if (p.ksplit > 1) {
+        const long long threads = M * (N / 4);
+        hipLaunchKernelGGL(igemm_splitk_epilogue_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, p);
+    }
     return check_launch("pu_conv_igemm");
 }
 
-extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* mode) {
+extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
+    if (!a || a->batch <= 0 || a->out_h <= 0 || a->out_w <= 0 || a->n <= 0 || a->k_pad <= 0) return 0;
+    const long long M = (long long)a->batch * a->out_h * a->out_w;
+    int bm, bn, ks, tp;
+    choose_tile(M, a->n, &bm, &bn);
+    plan_split(a, M, bm, bn, &ks, &tp);
+    return split_bytes(M, a->n, ks);
+}
+
+extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* mode, int* ksplit) {
     PU_REQUIRE(a && bm && bn && mode, "pu_conv_igemm_tile: null args");
     const long long M = (long long)a->batch * a->out_h * a->out_w;
     choose_tile(M, a->n, bm, bn);
     *mode = choose_mode(a->c0, a->c1);
+    if (ksplit) {
+        int ks, tp;
+        plan_split(a, M, *bm, *bn, &ks, &tp);
+        *ksplit = (ks > 1 && a->workspace && a->ws_bytes >= split_bytes(M, a->n, ks)) ? ks : 1;
+    }
     return PU_OK;
 }

@@ -30,6 +30,7 @@ struct WgradParams {
     float* slab;
     int mps;  // pixel rows per split (multiple of WG_BM)
     int gx, gy;  // k-tiles, n-tiles
+    int Kcp;     // slab row stride (Kc rounded up to 4)
     FastDiv dWo, dHo, dC, dKw;
 };
 
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
     }
 
     // ---- partial tile -> slab[z][n][k]
-    float* slab = p.slab + (long long)tz * p.Nr * p.Kc;
+    float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
 #pragma unroll
     for (int i = 0; i < FN; ++i) {
 #pragma unroll
@@ -218,7 +219,191 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int n = n_blk + wn * (BN / WN) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (n < p.Nr) slab[(long long)n * p.Kc + k] = acc[i][j][r];
+                if (n < p.Nr) slab[(long long)n * p.Kcp + k] = acc[i][j][r];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------ direct-to-LDS variant
+// C % 4 == 0: P and Q tiles are fetched with global_load_lds_dwordx4 into row-major LDS images
+// ([16 rows][BN] and [16 rows][BK]); the MFMA operands are ds_read_b32 of 32 consecutive floats
+// per half-wave (conflict-free).  Padding / out-of-image taps read a zero page.  Roles are
+// transposed (Q as the A operand) so each lane owns 4 consecutive k of one n and the partial tile
+// is stored as float4 into a Kcp-strided slab.  The bias is not an extra GEMM column/row (that
+// costs a whole extra tile whenever K or N is a multiple of the tile): the k-tile-0 blocks
+// (mode 1) or n-tile-0 blocks (mode 2) column-sum the staged P / Q image out of LDS on the VALU
+// and write the partial into slab column K / row N.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+__device__ __attribute__((aligned(16))) float g_wg_zero16[4] = {0.f, 0.f, 0.f, 0.f};
+
+template <int BN, int BK, int WN, int WK, int NBUF>
+__global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
+    constexpr int FN = BN / WN / 32;
+    constexpr int FK = BK / WK / 32;
+    constexpr int P_ROWS = 256 / BN;              // rows per 1 KB glds instruction
+    constexpr int P_LD = WG_BM / P_ROWS / 4;      // glds per wave per stage
+    constexpr int Q_LD = WG_BM * BK / 1024;       // Q instructions may straddle rows (BK = 192)
+    constexpr int G = P_LD + Q_LD;
+    constexpr int STAGE = WG_BM * (BN + BK);
+    static_assert(WN * WK == 4 && P_LD >= 1 && Q_LD >= 1 && 256 % BN == 0 && (WG_BM * BK) % 1024 == 0, "tile");
+
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave % WN, wk = wave / WN;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % p.gx;
+    const int tyz = tile / p.gx;
+    const int ty = tyz % p.gy;
+    const int tz = tyz / p.gy;
+    const int n_blk = ty * BN;
+    const int k_blk = tx * BK;
+    const int m_begin = tz * p.mps;
+    const int m_end = min(p.M, m_begin + p.mps);
+
+    // P lane geometry: column n (fixed), row delta within the instruction
+    const int p_col = (lane % (BN / 4)) * 4;
+    const int p_dr = lane / (BN / 4);
+    const int pn = n_blk + p_col;
+    const bool p_in = pn < p.N;
+    // Q lane geometry per instruction j: image float offset (wave*Q_LD + j)*256 + 4*lane ->
+    // (uniform first row q_row0, lane row delta, column k -> tap offsets and channel)
+    int q_row0[Q_LD], q_dr[Q_LD], q_r[Q_LD], q_s[Q_LD], q_cs[Q_LD];
+    const float* q_ptr[Q_LD];
+#pragma unroll
+    for (int j = 0; j < Q_LD; ++j) {
+        const int base = (wave * Q_LD + j) * 256;
+        const int off = base + 4 * lane;
+        q_row0[j] = base / BK;
+        q_dr[j] = off / BK - q_row0[j];
+        const int qk = k_blk + off % BK;
+        q_r[j] = 0; q_s[j] = 0; q_cs[j] = 0; q_ptr[j] = nullptr;
+        if (qk < p.K) {
+            const int tap = fdiv(qk, p.dC);
+            const int c = qk - tap * p.C;
+            q_r[j] = fdiv(tap, p.dKw);
+            q_s[j] = tap - q_r[j] * p.kw;
+            const bool first = c < p.c0;
+            q_ptr[j] = first ? p.src0 + c : p.src1 + (c - p.c0);
+            q_cs[j] = first ? p.c0 : p.c1;
+        }
+    }
+
+    auto issue = [&](int m0, int slot) {
+        float* ps = lds + slot * STAGE;
+        float* qs = ps + WG_BM * BN;
+#pragma unroll
+        for (int j = 0; j < P_LD; ++j) {
+            const int row0 = (wave * P_LD + j) * P_ROWS;
+            const int m = m0 + row0 + p_dr;
+            const float* g = g_wg_zero16;
+            if (m < m_end && p_in) g = p.P + (long long)m * p.N + pn;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(ps + row0 * BN), 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < Q_LD; ++j) {
+            const int mu = m0 + q_row0[j];   // wave-uniform: decomposed on the scalar unit
+            const int tu = fdiv(mu, p.dWo);
+            const int wou = mu - tu * p.Wo;
+            const int bu = fdiv(tu, p.dHo);
+            const int hou = tu - bu * p.Ho;
+            int wo = wou + q_dr[j], ho = hou, b = bu;
+            while (wo >= p.Wo) {
+                wo -= p.Wo;
+                if (++ho >= p.Ho) { ho = 0; ++b; }
+            }
+            const float* g = g_wg_zero16;
+            if (mu + q_dr[j] < m_end && q_ptr[j]) {
+                const int hi = ho * p.stride - p.pad + q_r[j], wi = wo * p.stride - p.pad + q_s[j];
+                if ((unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
+                    g = q_ptr[j] + ((long long)b * p.Hi * p.Wi + (long long)hi * p.Wi + wi) * q_cs[j];
+            }
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(qs + (wave * Q_LD + j) * 256), 16, 0, 0);
+        }
+    };
+
+    f32x16 acc[FK][FN];
+#pragma unroll
+    for (int i = 0; i < FK; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int a_col0 = wn * (BN / WN) + lr;   // n columns this lane reads from P
+    const int b_col0 = wk * (BK / WK) + lr;   // k columns this lane reads from Q
+    const int T = (m_end > m_begin) ? (m_end - m_begin + WG_BM - 1) / WG_BM : 0;
+
+    // bias column sums (block-uniform role): mode 1 sums P columns in k-tile 0, mode 2 Q columns in n-tile 0
+    const int bias_w = (p.bias_mode == 1 && tx == 0) ? BN : (p.bias_mode == 2 && ty == 0) ? BK : 0;
+    float bsum = 0.f;
+
+#pragma unroll
+    for (int s0 = 0; s0 < NBUF - 1; ++s0)
+        if (s0 < T) issue(m_begin + s0 * WG_BM, s0);
+
+    for (int t = 0; t < T; ++t) {
+        if (t + NBUF - 2 < T) {
+            if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        if (t + NBUF - 1 < T) issue(m_begin + (t + NBUF - 1) * WG_BM, (t + NBUF - 1) % NBUF);
+        const float* ps = lds + (t % NBUF) * STAGE;
+        const float* qs = ps + WG_BM * BN;
+        if (tid < bias_w) {   // one column per thread, all rows of the stage
+            const float* img = p.bias_mode == 1 ? ps : qs;
+#pragma unroll
+            for (int r = 0; r < WG_BM; ++r) bsum += img[r * bias_w + tid];
+        }
+#pragma unroll
+        for (int ks = 0; ks < WG_BM / 2; ++ks) {
+            const int row = ks * 2 + lh;
+            float fa[FN], fb[FK];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) fa[j] = ps[row * BN + a_col0 + j * 32];
+#pragma unroll
+            for (int i = 0; i < FK; ++i) fb[i] = qs[row * BK + b_col0 + i * 32];
+#pragma unroll
+            for (int i = 0; i < FK; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[i], fa[j], acc[i][j], 0, 0, 0);
+        }
+    }
+
+    // partial tile -> slab[z][n][k] (row stride Kcp, float4 over 4 consecutive k)
+    float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
+    if (tid < bias_w) {
+        if (p.bias_mode == 1) {
+            const int n = n_blk + tid;
+            if (n < p.N) slab[(long long)n * p.Kcp + p.K] = bsum;
+        } else {
+            const int k = k_blk + tid;
+            if (k < p.K) slab[(long long)p.N * p.Kcp + k] = bsum;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int n = n_blk + wn * (BN / WN) + j * 32 + lr;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int i = 0; i < FK; ++i) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = k_blk + wk * (BK / WK) + i * 32 + 8 * q + 4 * lh;
+                if (k >= p.K) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
             }
         }
     }
@@ -245,7 +430,7 @@ __global__ void wgrad_sum_splits_kernel(const float* __restrict__ slab, int spli
 
 // pass 2: sum the G groups (fixed order) and scatter to PyTorch's [n][c][kh][kw] + bias.
 // Threads [0, total) handle slab entries; threads [total, total + C) the ConvT bias (mode 2).
-__global__ void wgrad_finish_kernel(const double* __restrict__ part, int G, int Nr, int Kc, int N, int K, int C,
+__global__ void wgrad_finish_kernel(const double* __restrict__ part, int G, int Nr, int Kc, int N, int K, int C,  // Kc = slab row stride
                                     int kh, int kw, int bias_mode, float* __restrict__ dw, float* __restrict__ db,
                                     int accumulate) {
     const long long total = (long long)Nr * Kc;
@@ -276,10 +461,10 @@ __global__ void wgrad_finish_kernel(const double* __restrict__ part, int G, int 
 }
 
 struct WgradPlan {
-    int BN, BK, splits, mps, Nr, Kc, M, K, C, G;
-    bool qvec;
-    size_t slab_bytes() const { return (size_t)splits * Nr * Kc * sizeof(float); }
-    size_t part_bytes() const { return (size_t)G * Nr * Kc * sizeof(double); }
+    int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
+    bool qvec, dma;
+    size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
+    size_t part_bytes() const { return (size_t)G * Nr * Kcp * sizeof(double); }
     size_t ws_bytes() const { return ((slab_bytes() + 255) / 256) * 256 + part_bytes(); }
 };
 
@@ -298,16 +483,37 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->K = a->kh * a->kw * pl->C;
     pl->Nr = a->n + (a->bias_mode == 2 ? 1 : 0);
     pl->Kc = pl->K + (a->bias_mode == 1 ? 1 : 0);
+    pl->Kcp = (pl->Kc + 3) / 4 * 4;
     pl->qvec = (a->c0 % 4 == 0) && (a->c1 % 4 == 0);
     if (pl->qvec) {
         PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0, "pu_wgrad: sources must be 16-byte aligned");
     }
     PU_REQUIRE(((uintptr_t)a->rows & 15) == 0, "pu_wgrad: rows must be 16-byte aligned");
-    if (pl->Kc <= 64) { pl->BN = 64; pl->BK = 64; }
-    else if (pl->Nr <= 64) { pl->BN = 64; pl->BK = 256; }
-    else { pl->BN = 128; pl->BK = 128; }
-    const int tiles = ceil_div(pl->Nr, pl->BN) * ceil_div(pl->Kc, pl->BK);
-    int splits = ceil_div(768, tiles);
+#ifdef PU_NO_DMA
+    pl->dma = false;
+#else
+    pl->dma = pl->qvec;
+#endif
+    // the direct-to-LDS kernel tiles only the N x K GEMM (bias via LDS column sums); the
+    // register-staged kernel carries the bias as an extra ones column / row
+    const int ext_n = pl->dma ? a->n : pl->Nr;
+    const int ext_k = pl->dma ? pl->K : pl->Kc;
+    int occ;  // resident blocks per CU (LDS / VGPR limited, from the resource-usage report)
+    if (ext_k <= 64) { pl->BN = 64; pl->BK = 64; occ = pl->dma ? 6 : 7; }
+    else if (ext_n <= 64 && !pl->dma) { pl->BN = 64; pl->BK = 256; occ = 3; }
+    else if (ext_n <= 64) {
+        // BK 128 (4 resident blocks) unless 192 (3 resident) pads k less - e.g. K = 9 taps x 64
+        const bool b192 = ceil_div(ext_k, 192) * 192 < ceil_div(ext_k, 128) * 128;
+        pl->BN = 64; pl->BK = b192 ? 192 : 128; occ = b192 ? 3 : 4;
+    }
+    else { pl->BN = 128; pl->BK = 128; occ = pl->dma ? 3 : 4; }
+    pl->gx = ceil_div(ext_k, pl->BK);
+    pl->gy = ceil_div(ext_n, pl->BN);
+    const int tiles = pl->gx * pl->gy;
+    // one full round of resident blocks: a grid a few blocks past a multiple of the resident
+    // slots costs a whole extra round
+    const int slots = 256 * occ;
+    int splits = slots / tiles;
     int max_splits = ceil_div(M, 256);
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -348,7 +554,7 @@ extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes
         return fail(PU_ERR_WORKSPACE, "pu_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
 
     WgradParams p;
-    p.M = pl.M; p.N = a->n; p.Nr = pl.Nr; p.K = pl.K; p.Kc = pl.Kc; p.C = pl.C; p.c0 = a->c0; p.c1 = a->c1;
+    p.M = pl.M; p.N = a->n; p.Nr = pl.Nr; p.K = pl.K; p.Kc = pl.Kc; p.Kcp = pl.Kcp; p.C = pl.C; p.c0 = a->c0; p.c1 = a->c1;
     p.Hi = a->in_h; p.Wi = a->in_w; p.Ho = a->out_h; p.Wo = a->out_w;
     p.kw = a->kw; p.stride = a->stride; p.pad = a->pad;
     p.P = a->rows; p.src0 = a->src0; p.src1 = a->src1; p.bias_mode = a->bias_mode;
@@ -357,28 +563,37 @@ extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes
     p.dC = make_fastdiv(pl.C); p.dKw = make_fastdiv(a->kw);
 
     hipStream_t s = as_stream(stream);
-    p.gx = ceil_div(pl.Kc, pl.BK);
-    p.gy = ceil_div(pl.Nr, pl.BN);
+    p.gx = pl.gx;
+    p.gy = pl.gy;
     dim3 grid(p.gx * p.gy * pl.splits);
-#define PU_WG_LAUNCH(BN_, BK_, WN_, WK_)                                                              \
-    do {                                                                                               \
-        if (pl.qvec) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, true>), grid, dim3(256), 0, s, p);  \
-        else hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, false>), grid, dim3(256), 0, s, p);         \
-    } while (0)
-    if (pl.BK == 64) PU_WG_LAUNCH(64, 64, 2, 2);
-    else if (pl.BK == 256) PU_WG_LAUNCH(64, 256, 1, 4);
-    else PU_WG_LAUNCH(128, 128, 2, 2);
-#undef PU_WG_LAUNCH
+#define PU_WG_DMA(BN_, BK_, WN_, WK_) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3>), grid, dim3(256), 0, s, p)
+#define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
+    if (pl.dma) {
+        if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
+        else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
+        else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
+        else PU_WG_DMA(128, 128, 2, 2);
+    } else if (pl.qvec) {
+        if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, true);
+        else if (pl.BK == 256) PU_WG_REG(64, 256, 1, 4, true);
+        else PU_WG_REG(128, 128, 2, 2, true);
+    } else {
+        if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, false);
+        else if (pl.BK == 256) PU_WG_REG(64, 256, 1, 4, false);
+        else PU_WG_REG(128, 128, 2, 2, false);
+    }
+#undef PU_WG_DMA
+#undef PU_WG_REG
     st = check_launch("pu_wgrad (gemm)");
     if (st != PU_OK) return st;
 
-    const long long total = (long long)pl.Nr * pl.Kc;
+    const long long total = (long long)pl.Nr * pl.Kcp;
     double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
     hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
                        (const float*)workspace, pl.splits, total, pl.G, part);
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
     hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                       (const double*)part, pl.G, pl.Nr, pl.Kc, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode,
+                       (const double*)part, pl.G, pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode,
                        a->dweight, a->dbias, a->accumulate);
     return check_launch("pu_wgrad (reduce)");
 }

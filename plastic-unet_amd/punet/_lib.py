@@ -27,7 +27,8 @@ class ConvArgs(ctypes.Structure):
                 ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int),
                 ("src0", P), ("c0", c_int), ("src1", P), ("c1", c_int),
                 ("weight", P), ("k_pad", c_int), ("cgroup", c_int), ("n", c_int), ("bias", P),
-                ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int)]
+                ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int),
+                ("workspace", P), ("ws_bytes", c_size)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -57,8 +58,9 @@ SIGNATURES = [
     ("pu_last_error", ctypes.c_char_p, []),
     ("pu_device_info", c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_ll)]),
     ("pu_conv_igemm", c_int, [ctypes.POINTER(ConvArgs), P]),
+    ("pu_conv_igemm_workspace_bytes", c_size, [ctypes.POINTER(ConvArgs)]),
     ("pu_conv_igemm_tile", c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
-                                   ctypes.POINTER(c_int)]),
+                                   ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_wgrad_workspace_bytes", c_size, [ctypes.POINTER(WgradArgs)]),
     ("pu_wgrad", c_int, [ctypes.POINTER(WgradArgs), P, c_size, P]),
     ("pu_wgrad_tile", c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),

@@ -125,14 +125,19 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
-                 _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags)
+                 _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0)
+    L = lib()
+    nbytes = L.pu_conv_igemm_workspace_bytes(ctypes.byref(a))
+    if nbytes:     # split-K scratch from the caching allocator (stream-ordered reuse)
+        ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=dst0.device)
+        a.workspace, a.ws_bytes = ws.data_ptr(), nbytes
     if _PROF is None:
-        check(lib().pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
+        check(L.pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
         return
-    bm, bn, mode = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    lib().pu_conv_igemm_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(mode))
+    bm, bn, mode, ks = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    L.pu_conv_igemm_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(mode), ctypes.byref(ks))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "igemm<%dx%d,%s>" % (bm.value, bn.value, _MODES[mode.value])
+    tag = "igemm<%dx%d,%s%s>" % (bm.value, bn.value, _MODES[mode.value], ",k%d" % ks.value if ks.value > 1 else "")
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
         check(lib().pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
 

@@ -45,6 +45,29 @@ def test_invalid_arguments_return_errors_without_gpu():
         _lib.check(lib.pu_plastic_fwd(ctypes.byref(_lib.PlasticArgs()), None), "pu_plastic_fwd")
 
 
+def _conv(lib_mod, B, H, c, n, ws=None, ws_bytes=0):
+    A = 0x10000          # 16-byte aligned stand-in pointers: planning never dereferences them
+    return lib_mod.ConvArgs(B, H, H, H, H, 3, 3, 1, 1, A, c, None, 0, A, (9 * c + 15) // 16 * 16, 0, n, A,
+                            A, n, None, None, None, 1, ws, ws_bytes)
+
+
+def test_igemm_split_k_plan():
+    """Small pixel grids split K (fills the chip), large ones do not; without scratch no split."""
+    from punet import _lib
+    lib = _lib.load()
+    bm, bn, mode, ks = (ctypes.c_int() for _ in range(4))
+    bottom = _conv(_lib, 32, 8, 512, 512)                    # C2 8x8 level: 256 tiles of 64x64
+    nbytes = lib.pu_conv_igemm_workspace_bytes(ctypes.byref(bottom))
+    assert nbytes > 0 and nbytes % (32 * 8 * 8 * 512 * 4) == 0
+    lib.pu_conv_igemm_tile(ctypes.byref(bottom), *(ctypes.byref(v) for v in (bm, bn, mode, ks)))
+    assert ks.value == 1                                     # no workspace passed -> unsplit
+    with_ws = _conv(_lib, 32, 8, 512, 512, 0x20000, nbytes)
+    lib.pu_conv_igemm_tile(ctypes.byref(with_ws), *(ctypes.byref(v) for v in (bm, bn, mode, ks)))
+    assert ks.value == nbytes // (32 * 8 * 8 * 512 * 4) >= 2
+    top = _conv(_lib, 32, 128, 64, 64)                       # 2048 tiles: no split
+    assert lib.pu_conv_igemm_workspace_bytes(ctypes.byref(top)) == 0
+
+
 def test_header_structs_match_ctypes_layout():
     """Field order/size of the ctypes mirrors (a mismatch would corrupt every launch)."""
     from punet import _lib

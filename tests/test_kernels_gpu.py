@@ -48,7 +48,9 @@ CONV_CASES = [
     (2, 8, 8, 16, 16, 24),      # two sources (concat), N not a tile multiple
     (1, 8, 8, 8, 8, 8),         # two sources, vec4
     (2, 32, 32, 32, 0, 128),    # 128x128 tile
-    (1, 4, 4, 64, 64, 40),      # tiny M, 64x64 tile
+    (1, 4, 4, 64, 64, 40),      # tiny M, 64x64 tile, split-K (fwd + dgrad with the n0 split)
+    (2, 8, 8, 48, 0, 64),       # wgrad 64x128 tile, ragged last k-tile, bias column sums
+    (1, 8, 8, 64, 64, 32),      # wgrad 64x128 tile, two sources
 ]
 
 
@@ -87,7 +89,9 @@ def test_conv3x3_fwd_dgrad_wgrad(B, H, W, c0, c1, cout):
     assert_close(db, br.grad)
 
 
-@pytest.mark.parametrize("B,h,cin,cout", [(2, 4, 16, 16), (3, 8, 64, 64), (2, 8, 8, 8), (1, 16, 128, 128)])
+# (1, 4, 512, 64): tiny pixel grid, deep K -> split-K igemm for the shuffled forward and the dgrad
+@pytest.mark.parametrize("B,h,cin,cout", [(2, 4, 16, 16), (3, 8, 64, 64), (2, 8, 8, 8), (1, 16, 128, 128),
+                                          (1, 4, 512, 64)])
 def test_convT2x2(B, h, cin, cout):
     g = torch.Generator().manual_seed(h * 7 + cin)
     x = rnd(B, cin, h, h, g=g).relu().requires_grad_(True)
