@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-profile", action="store_true")
+    ap.add_argument("--no-oja", action="store_true", help="skip the Oja-update HBM benchmark")
     return ap.parse_args()
 
 
@@ -202,7 +203,7 @@ def main():
                 pass
 
     oja = None
-    if rank == 0:
+    if rank == 0 and not args.no_oja:
         oja = oja_update_bench(K, B, S, device)
 
     cpu = None

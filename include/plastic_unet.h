@@ -136,6 +136,10 @@ size_t pu_wgrad_workspace_bytes(const pu_wgrad_args* a);
 /* the tile (bn x bk), loader (qvec) and pixel-row split count pu_wgrad would use */
 int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec, int* splits);
 int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);
+/* pu_wgrad in two launches-worth of phases for per-kernel timing: phase 1 = the split-K GEMM
+ * (partials into the workspace), phase 2 = the fixed-order reduction + scatter; 1 then 2 on the
+ * same stream == pu_wgrad */
+int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, int phase, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Layout helpers

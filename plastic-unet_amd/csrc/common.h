@@ -58,8 +58,8 @@ inline FastDiv make_fastdiv(uint32_t d) {
 }
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
-    if (f.d == 1) return x;
-    // q = (x + umulhi(x, mul_lo)) >> l  where mul = 2^32 + mul_lo ;  x < 2^31 so no overflow
+    // q = (x + umulhi(x, mul_lo)) >> l  where mul = 2^32 + mul_lo ;  x < 2^31 so no overflow.
+    // Branch-free: d == 1 has mul_lo = 0, l = 0 (keeps hot loops one basic block).
     uint32_t hi = __umulhi(x, f.mul);
     return (hi + x) >> f.shift;
 }

@@ -435,28 +435,25 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
 
     const int t0 = kz * p.t_per;
     const int T = min(p.k_pad / IG_BK - t0, p.t_per);
+    // issue(tl): loads of local stage tl into ring slot `slot`.  Branch-free (selects only) so the
+    // main loop stays one basic block; stages tl >= T load the zero page (never read).
     auto issue = [&](int tl, int slot) {
-        const int t = t0 + tl;
+        const bool live = tl < T;
+        const int t = t0 + (live ? tl : 0);
         const int k0 = t * IG_BK;
-        int tap, c;
-        if (p.cgroup) {
-            const int per = p.cgroup >> 4;
-            const int tg = per == 2 ? (t >> 1) : t;
-            const int h = per == 2 ? (t & 1) : 0;
-            const int g = fdiv(tg, p.dTaps);
-            tap = tg - g * p.taps;
-            c = g * p.cgroup + h * 16;
-        } else {
-            tap = fdiv(k0, p.dC);
-            c = k0 - tap * p.C;
-        }
+        const bool two = p.cgroup == 32;
+        const int tg = two ? (t >> 1) : t;
+        const int g = fdiv(tg, p.dTaps);
+        const int tap_n = fdiv(k0, p.dC);
+        const int tap = p.cgroup ? tg - g * p.taps : tap_n;
+        const int c = p.cgroup ? g * p.cgroup + (two ? (t & 1) * 16 : 0) : k0 - tap_n * p.C;
         const int r = fdiv(tap, p.dKw);
         const int s = tap - r * p.kw;
         const bool first = c < p.c0;
         const float* src = first ? p.src0 : p.src1;
         const int cs = first ? p.c0 : p.c1;
         const long long off = (long long)(r * p.Wi + s) * cs + (first ? c : c - p.c0);
-        const unsigned bit = (k0 < p.K) ? (1u << tap) : 0u;
+        const unsigned bit = (live && k0 < p.K) ? (1u << tap) : 0u;
         float* a_slot = lds + slot * STAGE;
         float* b_slot = a_slot + BM * 16;
 #pragma unroll
@@ -467,7 +464,7 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
         }
 #pragma unroll
         for (int j = 0; j < B_LD; ++j) {
-            const float* g = wrow[j] ? wrow[j] + k0 : g_zero16;
+            const float* g = (live && wrow[j]) ? wrow[j] + k0 : g_zero16;
             __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(b_slot + (wave * (BN / 4) + 16 * j) * 16),
                                              16, 0, 0);
         }
@@ -486,38 +483,45 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
     const int swz = (lr >> 2) & 3;   // ((row >> 2) & 3) of every row this lane reads
 
 #pragma unroll
-    for (int s0 = 0; s0 < NBUF - 1; ++s0)
-        if (s0 < T) issue(s0, s0);
+    for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(s0, s0);
 
     for (int t = 0; t < T; ++t) {
         // stage t has landed (own loads) when at most the younger stages' G loads are pending
-        if (t + NBUF - 2 < T) {
-            if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        // (every iteration issues one stage, past the end too, so the count is constant)
+        if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
         __builtin_amdgcn_s_barrier();   // everyone's stage-t loads landed; slot (t-1) is free
-        if (t + NBUF - 1 < T) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
         const float* a = lds + (t % NBUF) * STAGE;
         const float* b = a + BM * 16;
+        // both k-halves' operands up front (the second half's reads land under the first
+        // half's MFMAs); the next stage's loads are issued between the halves so their address
+        // arithmetic overlaps MFMA execution instead of delaying the first MFMA of the stage
+        f32x4 fa[2][FM], fb[2][FN];
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const int pos = ((kk * 2 + lh) ^ swz) * 4;
-            f32x4 fa[FM], fb[FN];
 #pragma unroll
-            for (int i = 0; i < FM; ++i) fa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos);
+            for (int i = 0; i < FM; ++i) fa[kk][i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos);
 #pragma unroll
-            for (int j = 0; j < FN; ++j) fb[j] = *reinterpret_cast<const f32x4*>(b + (b_row0 + j * 32) * 16 + pos);
+            for (int j = 0; j < FN; ++j) fb[kk][j] = *reinterpret_cast<const f32x4*>(b + (b_row0 + j * 32) * 16 + pos);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
                 for (int i = 0; i < FM; ++i)
 #pragma unroll
                     for (int j = 0; j < FN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[kk][j][s], fa[kk][i][s], acc[i][j], 0, 0, 0);
+            if (kk == 0) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
         }
+        // keep all operand reads ahead of the MFMAs (the default scheduler sinks the second
+        // half's reads behind the first half's MFMAs, exposing their latency)
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * (FM + FN), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 * FM * FN, 0);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the past-the-end zero-page loads
     if (p.ksplit == 1) {
         epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
         return;
@@ -573,10 +577,16 @@ static void launch_mode(int mode, const IgemmParams& p, dim3 grid, hipStream_t s
 static int blocks_for(long long M, int N, int bm, int bn) { return ceil_div(M, bm) * ceil_div(N, bn); }
 
 // tile choice: the largest tile that still gives >= ~2 blocks per CU (256 CUs)
+#ifndef PU_IG_NBUF
+#define PU_IG_NBUF 3    // exploration knob: LDS ring depth of the direct-to-LDS kernel (3 or 4)
+#endif
+#ifndef PU_N64_BM
+#define PU_N64_BM 256   // exploration knob (tools/variants): M tile for N <= 64 layers
+#endif
 static void choose_tile(long long M, int N, int* bm, int* bn) {
     const int target = 480;
     if (N <= 64) {
-        if (blocks_for(M, N, 256, 64) >= target) { *bm = 256; *bn = 64; }
+        if (PU_N64_BM == 256 && blocks_for(M, N, 256, 64) >= target) { *bm = 256; *bn = 64; }
         else if (blocks_for(M, N, 128, 64) >= target) { *bm = 128; *bn = 64; }
         else { *bm = 64; *bn = 64; }
     } else {
@@ -685,10 +695,10 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     p.part = (float*)a->workspace;
     const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
     if (mode == LOAD_CHUNK16 && !PU_NO_DMA) {
-        if (bm == 256) hipLaunchKernelGGL((igemm_dma_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
-        else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 128, 2, 2, 3>), grid, dim3(256), 0, s, p);
-        else if (bm == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((igemm_dma_kernel<64, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
+        if (bm == 256) hipLaunchKernelGGL((igemm_dma_kernel<256, 64, 4, 1, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
+        else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 128, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
+        else if (bm == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 64, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((igemm_dma_kernel<64, 64, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
     } else if (bm == 256) launch_mode<256, 64, 4, 1>(mode, p, grid, s);
     else if (bm == 128 && bn == 128) launch_mode<128, 128, 2, 2>(mode, p, grid, s);
     else if (bm == 128) launch_mode<128, 64, 2, 2>(mode, p, grid, s);

@@ -312,11 +312,14 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
             const int wou = mu - tu * p.Wo;
             const int bu = fdiv(tu, p.dHo);
             const int hou = tu - bu * p.Ho;
-            int wo = wou + q_dr[j], ho = hou, b = bu;
-            while (wo >= p.Wo) {
-                wo -= p.Wo;
-                if (++ho >= p.Ho) { ho = 0; ++b; }
-            }
+            // lane delta with carry, branch-free (keeps the main loop one basic block)
+            int wo = wou + q_dr[j];
+            const int cw = fdiv(wo, p.dWo);
+            wo -= cw * p.Wo;
+            int ho = hou + cw;
+            const int ch = fdiv(ho, p.dHo);
+            ho -= ch * p.Ho;
+            const int b = bu + ch;
             const float* g = g_wg_zero16;
             if (mu + q_dr[j] < m_end && q_ptr[j]) {
                 const int hi = ho * p.stride - p.pad + q_r[j], wi = wo * p.stride - p.pad + q_s[j];
@@ -343,41 +346,49 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
     const int bias_w = (p.bias_mode == 1 && tx == 0) ? BN : (p.bias_mode == 2 && ty == 0) ? BK : 0;
     float bsum = 0.f;
 
+    // every iteration issues one stage (past m_end: zero page), so the counted wait is constant
 #pragma unroll
-    for (int s0 = 0; s0 < NBUF - 1; ++s0)
-        if (s0 < T) issue(m_begin + s0 * WG_BM, s0);
+    for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(m_begin + s0 * WG_BM, s0);
 
     for (int t = 0; t < T; ++t) {
-        if (t + NBUF - 2 < T) {
-            if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
         __builtin_amdgcn_s_barrier();
-        if (t + NBUF - 1 < T) issue(m_begin + (t + NBUF - 1) * WG_BM, (t + NBUF - 1) % NBUF);
         const float* ps = lds + (t % NBUF) * STAGE;
         const float* qs = ps + WG_BM * BN;
+        // the whole stage's operands up front ((FN+FK)*8 VGPRs): the reads of step ks+1.. land
+        // under the MFMAs of step ks instead of a lgkmcnt(0) bubble before every step
+        float fa[WG_BM / 2][FN], fb[WG_BM / 2][FK];
+#pragma unroll
+        for (int ks = 0; ks < WG_BM / 2; ++ks) {
+            const int row = ks * 2 + lh;
+#pragma unroll
+            for (int j = 0; j < FN; ++j) fa[ks][j] = ps[row * BN + a_col0 + j * 32];
+#pragma unroll
+            for (int i = 0; i < FK; ++i) fb[ks][i] = qs[row * BK + b_col0 + i * 32];
+        }
+#pragma unroll
+        for (int ks = 0; ks < WG_BM / 2; ++ks) {
+#pragma unroll
+            for (int i = 0; i < FK; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[ks][i], fa[ks][j], acc[i][j], 0, 0, 0);
+            // next stage's loads mid-stage: address arithmetic overlaps the MFMAs
+            if (ks == 1) issue(m_begin + (t + NBUF - 1) * WG_BM, (t + NBUF - 1) % NBUF);
+        }
+        // pin the order the default scheduler undoes (it sinks each read next to its MFMA):
+        // all operand reads of the stage, then the MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, (WG_BM / 2) * (FN + FK), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, (WG_BM / 2) * FN * FK, 0);
+        // bias column sums after the MFMA block (a divergent branch here does not split it)
         if (tid < bias_w) {   // one column per thread, all rows of the stage
             const float* img = p.bias_mode == 1 ? ps : qs;
 #pragma unroll
             for (int r = 0; r < WG_BM; ++r) bsum += img[r * bias_w + tid];
         }
-#pragma unroll
-        for (int ks = 0; ks < WG_BM / 2; ++ks) {
-            const int row = ks * 2 + lh;
-            float fa[FN], fb[FK];
-#pragma unroll
-            for (int j = 0; j < FN; ++j) fa[j] = ps[row * BN + a_col0 + j * 32];
-#pragma unroll
-            for (int i = 0; i < FK; ++i) fb[i] = qs[row * BK + b_col0 + i * 32];
-#pragma unroll
-            for (int i = 0; i < FK; ++i)
-#pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[i], fa[j], acc[i][j], 0, 0, 0);
-        }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drain the past-the-end zero-page loads
 
     // partial tile -> slab[z][n][k] (row stride Kcp, float4 over 4 consecutive k)
     float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
@@ -428,9 +439,11 @@ __global__ void wgrad_sum_splits_kernel(const float* __restrict__ slab, int spli
     part[(long long)g * total + idx] = (s0 + s1) + (s2 + s3);
 }
 
-// pass 2: sum the G groups (fixed order) and scatter to PyTorch's [n][c][kh][kw] + bias.
+// pass 2: sum the G groups (fixed order, fp64) and scatter to PyTorch's [n][c][kh][kw] + bias.
 // Threads [0, total) handle slab entries; threads [total, total + C) the ConvT bias (mode 2).
-__global__ void wgrad_finish_kernel(const double* __restrict__ part, int G, int Nr, int Kc, int N, int K, int C,  // Kc = slab row stride
+// T = double: the G pass-1 partials;  T = float: the slab itself (G = splits, single pass).
+template <typename T>
+__global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, int Kc, int N, int K, int C,  // Kc = slab row stride
                                     int kh, int kw, int bias_mode, float* __restrict__ dw, float* __restrict__ db,
                                     int accumulate) {
     const long long total = (long long)Nr * Kc;
@@ -440,7 +453,7 @@ __global__ void wgrad_finish_kernel(const double* __restrict__ part, int G, int 
         const int k = int(idx - (long long)n * Kc);
         if (n >= N) return;
         double s = 0.0;
-        for (int g = 0; g < G; ++g) s += part[(long long)g * total + idx];
+        for (int g = 0; g < G; ++g) s += (double)part[(long long)g * total + idx];
         const float v = (float)s;
         if (k < K) {
             const int tap = k / C, c = k - tap * C;
@@ -454,7 +467,7 @@ __global__ void wgrad_finish_kernel(const double* __restrict__ part, int G, int 
         const int c = int(idx - total);
         double s = 0.0;
         for (int t = 0; t < kh * kw; ++t)
-            for (int g = 0; g < G; ++g) s += part[(long long)g * total + (long long)N * Kc + t * C + c];
+            for (int g = 0; g < G; ++g) s += (double)part[(long long)g * total + (long long)N * Kc + t * C + c];
         const float v = (float)s;
         db[c] = accumulate ? db[c] + v : v;
     }
@@ -464,7 +477,7 @@ struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
     bool qvec, dma;
     size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
-    size_t part_bytes() const { return (size_t)G * Nr * Kcp * sizeof(double); }
+    size_t part_bytes() const { return G > 1 ? (size_t)G * Nr * Kcp * sizeof(double) : 0; }
     size_t ws_bytes() const { return ((slab_bytes() + 255) / 256) * 256 + part_bytes(); }
 };
 
@@ -520,7 +533,16 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     int mps = ceil_div(ceil_div(M, splits), WG_BM) * WG_BM;
     pl->mps = mps;
     pl->splits = ceil_div(M, mps);
-    pl->G = pl->splits < 16 ? pl->splits : 16;
+    // reduction groups: one pass (G = 1, each thread sums every split of its entry) when the slab
+    // has enough entries to fill the chip; otherwise G groups of >= 8 splits each, then G partials
+    {
+        const long long total = (long long)pl->Nr * pl->Kcp;
+        int G = (int)ceil_div(262144LL, total);
+        const int by_len = ceil_div(pl->splits, 8);
+        if (G > by_len) G = by_len;
+        if (G > 16) G = 16;
+        pl->G = G < 1 ? 1 : G;
+    }
     return PU_OK;
 }
 
@@ -546,6 +568,11 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
 }
 
 extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes, void* stream) {
+    return pu_wgrad_phase(a, workspace, ws_bytes, 3, stream);
+}
+
+extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws_bytes, int phase, void* stream) {
+    PU_REQUIRE(phase >= 1 && phase <= 3, "pu_wgrad_phase: phase %d", phase);
     WgradPlan pl;
     int st = plan_wgrad(a, &pl);
     if (st != PU_OK) return st;
@@ -566,34 +593,44 @@ extern "C" int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t ws_bytes
     p.gx = pl.gx;
     p.gy = pl.gy;
     dim3 grid(p.gx * p.gy * pl.splits);
+    if (phase & 1) {
 #define PU_WG_DMA(BN_, BK_, WN_, WK_) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3>), grid, dim3(256), 0, s, p)
 #define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
-    if (pl.dma) {
-        if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
-        else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
-        else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
-        else PU_WG_DMA(128, 128, 2, 2);
-    } else if (pl.qvec) {
-        if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, true);
-        else if (pl.BK == 256) PU_WG_REG(64, 256, 1, 4, true);
-        else PU_WG_REG(128, 128, 2, 2, true);
-    } else {
-        if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, false);
-        else if (pl.BK == 256) PU_WG_REG(64, 256, 1, 4, false);
-        else PU_WG_REG(128, 128, 2, 2, false);
-    }
+        if (pl.dma) {
+            if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
+            else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
+            else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
+            else PU_WG_DMA(128, 128, 2, 2);
+        } else if (pl.qvec) {
+            if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, true);
+            else if (pl.BK == 256) PU_WG_REG(64, 256, 1, 4, true);
+            else PU_WG_REG(128, 128, 2, 2, true);
+        } else {
+            if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, false);
+            else if (pl.BK == 256) PU_WG_REG(64, 256, 1, 4, false);
+            else PU_WG_REG(128, 128, 2, 2, false);
+        }
 #undef PU_WG_DMA
 #undef PU_WG_REG
-    st = check_launch("pu_wgrad (gemm)");
-    if (st != PU_OK) return st;
+        st = check_launch("pu_wgrad (gemm)");
+        if (st != PU_OK) return st;
+    }
+    if (!(phase & 2)) return PU_OK;
 
     const long long total = (long long)pl.Nr * pl.Kcp;
-    double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
-    hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
-                       (const float*)workspace, pl.splits, total, pl.G, part);
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
-    hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
-                       (const double*)part, pl.G, pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode,
-                       a->dweight, a->dbias, a->accumulate);
+    const dim3 fgrid((unsigned)((threads + 255) / 256));
+    if (pl.G == 1) {
+        hipLaunchKernelGGL(wgrad_finish_kernel<float>, fgrid, dim3(256), 0, s, (const float*)workspace, pl.splits,
+                           pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,
+                           a->accumulate);
+    } else {
+        double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
+        hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
+                           (const float*)workspace, pl.splits, total, pl.G, part);
+        hipLaunchKernelGGL(wgrad_finish_kernel<double>, fgrid, dim3(256), 0, s, (const double*)part, pl.G, pl.Nr,
+                           pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,
+                           a->accumulate);
+    }
     return check_launch("pu_wgrad (reduce)");
 }

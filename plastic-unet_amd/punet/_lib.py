@@ -63,6 +63,7 @@ SIGNATURES = [
                                    ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_wgrad_workspace_bytes", c_size, [ctypes.POINTER(WgradArgs)]),
     ("pu_wgrad", c_int, [ctypes.POINTER(WgradArgs), P, c_size, P]),
+    ("pu_wgrad_phase", c_int, [ctypes.POINTER(WgradArgs), P, c_size, c_int, P]),
     ("pu_wgrad_tile", c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),

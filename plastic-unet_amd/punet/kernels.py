@@ -162,8 +162,11 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
     M = batch * out_hw[0] * out_hw[1]
     tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, "vec4" if qv.value else "scalar")
+    # the GEMM and the split reduction timed apart (they are separate kernels in rocprof too)
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
-        check(L.pu_wgrad(ctypes.byref(a), ws.data_ptr(), nbytes, _stream()), "pu_wgrad")
+        check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 1, _stream()), "pu_wgrad_phase")
+    with _Rec("wgrad_reduce", nbytes=float(nbytes)):
+        check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 2, _stream()), "pu_wgrad_phase")
 
 
 def pack_weight(w, mode, k_pad, out=None, cgroup=0):
