@@ -70,16 +70,21 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
  *             k = (g*taps + tap)*cgroup + (c % cgroup), g = c / cgroup (channel-group-major: the
  *             taps of one channel group are consecutive K stages, so their shifted re-reads of the
  *             same pixels hit L2).  Requires c0 % cgroup == 0 and c1 % cgroup == 0.
- * Epilogue per element: v = acc (+ bias) ; RELU: v = max(v,0) ; mask: v *= (mask > 0) ;
- *   ACCUM: dst += v else dst = v.  Columns [0,n0) go to dst0 (NHWC, n0 channels), [n0,n) to
- *   dst1 (NHWC, n-n0 channels).  SHUFFLE2: n = (2i+j)*co + c is stored at pixel (2ho+i, 2wo+j)
- *   of a (2*out_h, 2*out_w) NHWC grid with co = n/4 channels and bias[c] (ConvTranspose2d 2x2 s2).
+ * Epilogue per element: v = acc (+ bias) (+ resid, RESID) ; RELU: v = max(v,0) ;
+ *   mask: v *= (mask > 0) ; ACCUM: dst += v else dst = v.  Columns [0,n0) go to dst0 (NHWC, n0
+ *   channels), [n0,n) to dst1 (NHWC, n-n0 channels).  RESID: resid is an NHWC tensor shaped like
+ *   dst0 (requires n0 == n, no SHUFFLE2) - the residual add of unet_p_res.py:188 and its backward.
+ *   SHUFFLE2: n = (2i+j)*co + c is stored at pixel (2ho+i-shuf_off, 2wo+j-shuf_off) of a
+ *   (shuf_h, shuf_w) NHWC grid (0 -> 2*out_h, 2*out_w), co = n/4 channels, bias[c]; pixels
+ *   outside the grid are dropped.  ConvTranspose2d 2x2 s2: k=1, shuf_off=0.  ConvTranspose2d 3x3
+ *   s2 p0 (+ the crop of row/col 0, unet_p_res.py:207-217): k=2, pad=1, out grid (h+1)x(w+1),
+ *   weight packed PU_PACK_CONVT3_FWD, shuf_off = 1 (crop) or 0, shuf_h/w = the kept extent.
  * workspace (optional): when the M x N tile grid cannot fill the chip (small pixel grids: the
  *   8x8 / 16x16 levels of the U-Net) and ws_bytes >= pu_conv_igemm_workspace_bytes(a), K is split
  *   over ksplit blocks per tile; the partial tiles go to the workspace and a second kernel sums
  *   them in fixed split order (deterministic) and runs the epilogue above.  NULL -> no split.
  * ------------------------------------------------------------------------------------------- */
-enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4 };
+enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8 };
 
 typedef struct {
     int batch;
@@ -97,6 +102,8 @@ typedef struct {
     const float* mask1;
     int flags;
     void* workspace; size_t ws_bytes;
+    const float* resid;
+    int shuf_h, shuf_w, shuf_off;
 } pu_conv_args;
 
 int pu_conv_igemm(const pu_conv_args* a, void* stream);
@@ -148,13 +155,28 @@ enum {
     PU_PACK_CONV_FWD = 0,   /* w[O][I][R][S] -> p[o][(r*S+s)*I+i]                          */
     PU_PACK_CONV_DGRAD = 1, /* w[O][I][R][S] -> p[i][((R-1-r)*S+(S-1-s))*O+o] (flipped)    */
     PU_PACK_CONVT_FWD = 2,  /* w[I][O][R][S] -> p[(r*S+s)*O+o][i]                           */
-    PU_PACK_CONVT_DGRAD = 3 /* w[I][O][R][S] -> p[i][(r*S+s)*O+o]                           */
+    PU_PACK_CONVT_DGRAD = 3, /* w[I][O][R][S] -> p[i][(r*S+s)*O+o]                          */
+    PU_PACK_CONVT3_FWD = 4   /* w[I][O][3][3] -> p[(ph*2+pw)*O+o][(dh*2+dw)*I+i] = w[i][o][R(ph,dh)][R(pw,dw)]
+                              * with R(0,1)=0, R(0,0)=2, R(1,1)=1, R(1,0)=none (0): output (2p+ph)
+                              * of a 3x3 s2 transposed conv reads input (p-1+dh)               */
 };
 /* d0,d1 = first two dims of w; rows of p are k_pad floats wide (zero padded).  cgroup != 0 packs
  * the K axis channel-group-major (see pu_conv_args.cgroup) for the FWD/DGRAD/CONVT_DGRAD modes. */
 int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw,
                    int k_pad, int cgroup, void* stream);
 int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, void* stream);
+
+/* Dropout2d application (unet_p_res.py:209,248) on NHWC: y[b][p][c] = x[b][p][c] * scale[b][c]
+ * (scale 0 or 1/(1-p) per sample and channel); y may alias x.  The backward is the same call on
+ * the gradient. */
+int pu_channel_scale(const float* x, const float* scale, float* y, int batch, long long hw, int c,
+                     void* stream);
+
+/* Column sums of a row-major [rows][cols] matrix in fp64, fixed order (deterministic):
+ * out[c] (+)= sum_r x[r][c].  (ConvTranspose2d 3x3 bias gradient.) */
+size_t pu_column_sum_workspace_bytes(long long rows, int cols);
+int pu_column_sum(const float* x, long long rows, int cols, float* out, int accumulate,
+                  void* workspace, size_t workspace_bytes, void* stream);
 
 /* MaxPool2d(2) on NHWC (floor for odd sizes), first-max tie rule of ATen's CPU kernel.
  * bwd: dx[argmax] (+)= dy * (relu_mask ? (x[argmax] > 0) : 1); dx elsewhere: 0 (or kept if

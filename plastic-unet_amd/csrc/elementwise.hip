@@ -48,10 +48,21 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restric
                 int tap = row / d1, o = row - tap * d1;
                 v = w[((long long)k * d1 + o) * taps + tap];
             }
-        } else {                                 // PU_PACK_CONVT_DGRAD: -> [i][(r*S+s)*O+o]
+        } else if (mode == PU_PACK_CONVT_DGRAD) {  // -> [i][(r*S+s)*O+o]
             if (k < taps * d1) {
                 int tap = k / d1, o = k - tap * d1;
                 v = w[((long long)row * d1 + o) * taps + tap];
+            }
+        } else {                                 // PU_PACK_CONVT3_FWD: w[I=d0][O=d1][3][3]
+            // row = (ph*2+pw)*O + o, k = (dh*2+dw)*I + i ; tap index along one axis: R(0,1)=0,
+            // R(0,0)=2, R(1,1)=1, R(1,0) = none
+            if (k < 4 * d0) {
+                const int phw = row / d1, o = row - phw * d1;
+                const int dhw = k / d0, i = k - dhw * d0;
+                const int ph = phw >> 1, pw = phw & 1, dh = dhw >> 1, dw = dhw & 1;
+                const int r = ph == 0 ? (dh ? 0 : 2) : (dh ? 1 : -1);
+                const int q = pw == 0 ? (dw ? 0 : 2) : (dw ? 1 : -1);
+                if (r >= 0 && q >= 0) v = w[(((long long)i * d1 + o) * 3 + r) * 3 + q];
             }
         }
         p[idx] = v;
@@ -264,6 +275,67 @@ __global__ void column_sum_kernel(const float* __restrict__ partial, int nparts,
     }
 }
 
+// Dropout2d: y = x * scale[b][c] over NHWC
+template <bool VEC>
+__global__ void channel_scale_kernel(const float* __restrict__ x, const float* __restrict__ scale, float* y,
+                                     long long hw, int c, long long total) {
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        if (VEC) {
+            const int cq = c >> 2;
+            const long long pix = idx / cq;
+            const int c4 = int(idx - pix * cq) * 4;
+            const long long b = pix / hw;
+            f32x4 v = reinterpret_cast<const f32x4*>(x)[idx];
+            const float* sc = scale + b * c + c4;
+            v[0] *= sc[0]; v[1] *= sc[1]; v[2] *= sc[2]; v[3] *= sc[3];
+            reinterpret_cast<f32x4*>(y)[idx] = v;
+        } else {
+            const long long pix = idx / c;
+            const int ch = int(idx - pix * c);
+            y[idx] = x[idx] * scale[(pix / hw) * c + ch];
+        }
+    }
+}
+
+// column sums, pass 1: block q sums rows [q*rpb, (q+1)*rpb) of column chunk blockIdx.y (256 cols)
+// in fp64; threads = (row lane, column) with rl = 256 / cw row lanes
+__global__ void colsum_partial_kernel(const float* __restrict__ x, long long rows, int cols, long long rpb,
+                                      double* __restrict__ part) {
+    __shared__ double red[256];
+    const int c0 = blockIdx.y * 256;
+    const int cw = min(256, cols - c0);
+    const int rl = 256 / cw;
+    const int t = threadIdx.x;
+    const int col = t % cw, lane = t / cw;
+    double s = 0.0;
+    const long long r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+    if (lane < rl)
+        for (long long r = r0 + lane; r < r1; r += rl) s += (double)x[r * cols + c0 + col];
+    red[t] = s;
+    __syncthreads();
+    if (t < cw) {
+        double v = 0.0;
+        for (int l = 0; l < rl; ++l) v += red[l * cw + t];
+        part[(long long)blockIdx.x * cols + c0 + t] = v;
+    }
+}
+
+// pass 2: out[c] (+)= sum over the partial blocks in order
+__global__ void colsum_final_kernel(const double* __restrict__ part, int nparts, int cols, float* __restrict__ out,
+                                    int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    double s = 0.0;
+    for (int q = 0; q < nparts; ++q) s += part[(long long)q * cols + c];
+    out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+static int colsum_blocks(long long rows) {
+    long long b = (rows + 1023) / 1024;
+    return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
+
 static int grid_for(long long total, int block = 256, int cap = 8192) {
     long long g = (total + block - 1) / block;
     if (g > cap) g = cap;
@@ -283,13 +355,15 @@ extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, i
         const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;
         PU_REQUIRE(mode == PU_PACK_CONVT_FWD || Ck % cgroup == 0, "pu_pack_weight: %d channels not a multiple of cgroup %d", Ck, cgroup);
     }
-    PU_REQUIRE(mode >= 0 && mode <= 3, "pu_pack_weight: mode %d", mode);
+    PU_REQUIRE(mode >= 0 && mode <= 4, "pu_pack_weight: mode %d", mode);
+    PU_REQUIRE(mode != PU_PACK_CONVT3_FWD || (kh == 3 && kw == 3 && cgroup == 0), "pu_pack_weight: CONVT3_FWD is 3x3, tap-major");
     const int taps = kh * kw;
     int rows, kmin;
     switch (mode) {
         case PU_PACK_CONV_FWD: rows = d0; kmin = taps * d1; break;
         case PU_PACK_CONV_DGRAD: rows = d1; kmin = taps * d0; break;
         case PU_PACK_CONVT_FWD: rows = taps * d1; kmin = d0; break;
+        case PU_PACK_CONVT3_FWD: rows = 4 * d1; kmin = 4 * d0; break;
         default: rows = d0; kmin = taps * d1; break;
     }
     PU_REQUIRE(k_pad >= kmin, "pu_pack_weight: k_pad %d < %d", k_pad, kmin);
@@ -369,4 +443,38 @@ extern "C" int pu_outconv_bwd(const float* x, const float* w, const float* dy, f
                        relu_mask);
     hipLaunchKernelGGL(column_sum_kernel, dim3(c + 1), dim3(256), 0, as_stream(stream), part, blocks, c, dw, db);
     return check_launch("pu_outconv_bwd");
+}
+
+extern "C" int pu_channel_scale(const float* x, const float* scale, float* y, int batch, long long hw, int c,
+                                void* stream) {
+    PU_REQUIRE(x && scale && y && batch > 0 && hw > 0 && c > 0, "pu_channel_scale: bad args");
+    const bool vec = (c % 4 == 0) && (((uintptr_t)x | (uintptr_t)y) & 15) == 0;
+    const long long total = (long long)batch * hw * (vec ? c / 4 : c);
+    if (vec)
+        hipLaunchKernelGGL(channel_scale_kernel<true>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x,
+                           scale, y, hw, c, total);
+    else
+        hipLaunchKernelGGL(channel_scale_kernel<false>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x,
+                           scale, y, hw, c, total);
+    return check_launch("pu_channel_scale");
+}
+
+extern "C" size_t pu_column_sum_workspace_bytes(long long rows, int cols) {
+    if (rows <= 0 || cols <= 0) return 0;
+    return (size_t)colsum_blocks(rows) * cols * sizeof(double);
+}
+
+extern "C" int pu_column_sum(const float* x, long long rows, int cols, float* out, int accumulate, void* workspace,
+                             size_t ws_bytes, void* stream) {
+    PU_REQUIRE(x && out && rows > 0 && cols > 0, "pu_column_sum: bad args");
+    const size_t need = pu_column_sum_workspace_bytes(rows, cols);
+    if (!workspace || ws_bytes < need) return fail(PU_ERR_WORKSPACE, "pu_column_sum: workspace %zu < %zu", ws_bytes, need);
+    const int nb = colsum_blocks(rows);
+    const long long rpb = (rows + nb - 1) / nb;
+    double* part = (double*)workspace;
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb, (cols + 255) / 256), dim3(256), 0, as_stream(stream), x, rows,
+                       cols, rpb, part);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, as_stream(stream), part, nb, cols,
+                       out, accumulate);
+    return check_launch("pu_column_sum");
 }

@@ -51,6 +51,8 @@ struct IgemmParams {
     int vec_epi;            // float4 epilogue (channel counts % 4 == 0, 16-byte aligned buffers)
     int ksplit, t_per;      // split-K: blocks per tile and 16-wide K stages per split
     float* part;            // split-K partial tiles [ksplit][M][N]
+    const float* resid;     // RESID: NHWC tensor shaped like dst0, added before ReLU / mask
+    int shuf_h, shuf_w, shuf_off;   // SHUFFLE2 output grid and crop offset
     FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
 };
 
@@ -92,28 +94,43 @@ __device__ __forceinline__ f32x4 load_a4(const IgemmParams& p, int pb, int hb, i
     }
 }
 
-// Output pixel base of GEMM row m (SHUFFLE2: the top-left pixel of its 2x2 output block).
-__device__ __forceinline__ long long epi_pix(const IgemmParams& p, int m) {
-    if (!(p.flags & PU_EPI_SHUFFLE2)) return m;
+// Output position of GEMM row m: the pixel itself, or (SHUFFLE2) the batch row base b*shuf_h and
+// the top-left corner (2ho - off, 2wo - off) of its 2x2 output block.
+struct EpiRow {
+    long long pix;
+    int oh0, ow0;
+};
+
+__device__ __forceinline__ EpiRow epi_row(const IgemmParams& p, int m) {
+    if (!(p.flags & PU_EPI_SHUFFLE2)) return {m, 0, 0};
     const int t2 = fdiv(m, p.dWo);
     const int wo = m - t2 * p.Wo;
     const int bb = fdiv(t2, p.dHo);
     const int ho = t2 - bb * p.Ho;
-    return ((long long)bb * 2 * p.Ho + 2 * ho) * (2 * p.Wo) + 2 * wo;
+    return {(long long)bb * p.shuf_h, 2 * ho - p.shuf_off, 2 * wo - p.shuf_off};
 }
 
-// float4 epilogue of channels n..n+3 (n % 4 == 0, vec_epi) of the row with output pixel base pix.
-__device__ __forceinline__ void epi_store4(const IgemmParams& p, long long pix, int n, f32x4 v) {
+// SHUFFLE2 destination element offset of channel n of row r; false if cropped away
+__device__ __forceinline__ bool shuf_off(const IgemmParams& p, const EpiRow& r, int n, long long* off, int* c) {
+    const int co = p.N >> 2;
+    const int ij = fdiv(n, p.dCo);
+    *c = n - ij * co;
+    const int oh = r.oh0 + (ij >> 1), ow = r.ow0 + (ij & 1);
+    if ((unsigned)oh >= (unsigned)p.shuf_h || (unsigned)ow >= (unsigned)p.shuf_w) return false;
+    *off = ((r.pix + oh) * p.shuf_w + ow) * co + *c;
+    return true;
+}
+
+// float4 epilogue of channels n..n+3 (n % 4 == 0, vec_epi) of row r.
+__device__ __forceinline__ void epi_store4(const IgemmParams& p, const EpiRow& r, int n, f32x4 v) {
     float* dst;
     const float* msk;
     long long off;
     int nb;   // bias index of the first channel
+    const long long pix = r.pix;
     if (p.flags & PU_EPI_SHUFFLE2) {
-        const int co = p.N >> 2;
-        const int ij = fdiv(n, p.dCo);
-        const int c = n - ij * co;
-        off = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
-        dst = p.dst0; msk = p.mask0; nb = c;
+        if (!shuf_off(p, r, n, &off, &nb)) return;
+        dst = p.dst0; msk = p.mask0;
     } else if (n < p.n0) {
         off = pix * p.n0 + n;
         dst = p.dst0; msk = p.mask0; nb = n;
@@ -122,6 +139,7 @@ __device__ __forceinline__ void epi_store4(const IgemmParams& p, long long pix, 
         dst = p.dst1; msk = p.mask1; nb = n;
     }
     if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + nb);
+    if (p.resid) v += *reinterpret_cast<const f32x4*>(p.resid + off);
     if (p.flags & PU_EPI_RELU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -151,7 +169,8 @@ __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM 
     for (int i = 0; i < FM; ++i) {
         const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
         if (m >= p.M) continue;
-        const long long pix = epi_pix(p, m);
+        const EpiRow er = epi_row(p, m);
+        const long long pix = er.pix;
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
 #pragma unroll
@@ -162,7 +181,7 @@ __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM 
                     f32x4 v;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-                    epi_store4(p, pix, n, v);
+                    epi_store4(p, er, n, v);
                 } else {
                     // odd channel counts: per element (channel n+e may cross the n0 split)
 #pragma unroll
@@ -174,17 +193,14 @@ __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM 
                         long long o;
                         int bi = ne;
                         if (shuffle) {
-                            const int co = p.N >> 2;
-                            const int ij = fdiv(ne, p.dCo);
-                            const int c = ne - ij * co;
-                            o = (pix + (ij >> 1) * (2 * p.Wo) + (ij & 1)) * co + c;
-                            d = p.dst0; mk = p.mask0; bi = c;
+                            if (!shuf_off(p, er, ne, &o, &bi)) continue;
+                            d = p.dst0; mk = p.mask0;
                         } else if (ne < p.n0) {
                             o = pix * p.n0 + ne; d = p.dst0; mk = p.mask0;
                         } else {
                             o = pix * (p.N - p.n0) + (ne - p.n0); d = p.dst1; mk = p.mask1;
                         }
-                        float v = acc[i][j][4 * q + e] + (p.bias ? p.bias[bi] : 0.f);
+                        float v = acc[i][j][4 * q + e] + (p.bias ? p.bias[bi] : 0.f) + (p.resid ? p.resid[o] : 0.f);
                         if (relu) v = fmaxf(v, 0.f);
                         if (mk && !(mk[o] > 0.f)) v = 0.f;
                         if (accum) v += d[o];
@@ -557,7 +573,7 @@ __global__ __launch_bounds__(256) void igemm_splitk_epilogue_kernel(const IgemmP
     const float* src = p.part + (long long)m * p.N + n;
     f32x4 v = *reinterpret_cast<const f32x4*>(src);
     for (int z = 1; z < p.ksplit; ++z) v += *reinterpret_cast<const f32x4*>(src + z * mn);
-    epi_store4(p, epi_pix(p, m), n, v);
+    epi_store4(p, epi_row(p, m), n, v);
 }
 
 // ------------------------------------------------------------------------------------------ host
@@ -606,8 +622,9 @@ static bool vec_epilogue(const pu_conv_args* a) {
     const bool shuffle = a->flags & PU_EPI_SHUFFLE2;
     const int n0 = shuffle ? a->n : a->n0;
     const uintptr_t al = (uintptr_t)a->dst0 | (uintptr_t)a->dst1 | (uintptr_t)a->mask0 | (uintptr_t)a->mask1 |
-                         (uintptr_t)a->bias;
-    return (a->n % 4 == 0) && (n0 % 4 == 0) && (al & 15) == 0;
+                         (uintptr_t)a->bias | ((a->flags & PU_EPI_RESID) ? (uintptr_t)a->resid : 0);
+    // SHUFFLE2: 4 consecutive n stay inside one (i,j) block only when co = n/4 is a multiple of 4
+    return (a->n % 4 == 0) && (n0 % 4 == 0) && (al & 15) == 0 && (!shuffle || (a->n / 4) % 4 == 0);
 }
 
 // Split-K plan: when the M x N tile grid fills fewer than the resident block slots of the chip
@@ -648,8 +665,12 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     const int K = a->kh * a->kw * C;
     PU_REQUIRE(a->k_pad >= K && a->k_pad % IG_BK == 0, "pu_conv_igemm: k_pad %d must be >= %d and a multiple of 16", a->k_pad, K);
     const bool shuffle = a->flags & PU_EPI_SHUFFLE2;
+    if (a->flags & PU_EPI_RESID) {
+        PU_REQUIRE(a->resid && !shuffle && (a->n0 == a->n), "pu_conv_igemm: RESID needs resid, a single destination, no SHUFFLE2");
+    }
     if (shuffle) {
         PU_REQUIRE(a->n % 4 == 0, "pu_conv_igemm: SHUFFLE2 needs n %% 4 == 0");
+        PU_REQUIRE(a->shuf_off >= 0 && a->shuf_h >= 0 && a->shuf_w >= 0, "pu_conv_igemm: shuffle geometry");
     } else {
         PU_REQUIRE(a->n0 > 0 && a->n0 <= a->n, "pu_conv_igemm: n0 %d out of range", a->n0);
         PU_REQUIRE(a->n0 == a->n || a->dst1, "pu_conv_igemm: dst1 missing");
@@ -665,6 +686,10 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     p.src0 = a->src0; p.src1 = a->src1; p.wt = a->weight; p.bias = a->bias;
     p.dst0 = a->dst0; p.dst1 = a->dst1; p.mask0 = a->mask0; p.mask1 = a->mask1;
     p.n0 = shuffle ? a->n : a->n0; p.flags = a->flags;
+    p.resid = (a->flags & PU_EPI_RESID) ? a->resid : nullptr;
+    p.shuf_h = a->shuf_h ? a->shuf_h : 2 * a->out_h;
+    p.shuf_w = a->shuf_w ? a->shuf_w : 2 * a->out_w;
+    p.shuf_off = a->shuf_off;
     p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
     p.dC = make_fastdiv(C); p.dKw = make_fastdiv(a->kw); p.dCo = make_fastdiv(shuffle ? a->n / 4 : 1);
     p.taps = a->kh * a->kw;

@@ -17,8 +17,8 @@ LIB_PATH = os.environ.get("PLASTIC_UNET_LIB",
 c_int, c_ll, c_size, c_float, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
 P = ctypes.c_void_p
 
-PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2 = 1, 2, 4
-PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD = 0, 1, 2, 3
+PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID = 1, 2, 4, 8
+PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD, PU_PACK_CONVT3_FWD = 0, 1, 2, 3, 4
 PU_RULE_HEBB, PU_RULE_OJA = 0, 1
 
 
@@ -28,7 +28,8 @@ class ConvArgs(ctypes.Structure):
                 ("src0", P), ("c0", c_int), ("src1", P), ("c1", c_int),
                 ("weight", P), ("k_pad", c_int), ("cgroup", c_int), ("n", c_int), ("bias", P),
                 ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int),
-                ("workspace", P), ("ws_bytes", c_size)]
+                ("workspace", P), ("ws_bytes", c_size),
+                ("resid", P), ("shuf_h", c_int), ("shuf_w", c_int), ("shuf_off", c_int)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -68,6 +69,9 @@ SIGNATURES = [
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_nchw_to_nhwc", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    ("pu_channel_scale", c_int, [P, P, P, c_int, c_ll, c_int, P]),
+    ("pu_column_sum_workspace_bytes", c_size, [c_ll, c_int]),
+    ("pu_column_sum", c_int, [P, c_ll, c_int, P, c_int, P, c_size, P]),
     ("pu_maxpool2_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_maxpool2_bwd", c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_outconv_fwd", c_int, [P, P, P, P, c_ll, c_int, P]),

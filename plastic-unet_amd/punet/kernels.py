@@ -9,7 +9,7 @@ import torch
 
 from . import _lib
 from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticBwdArgs, AdamTensor, check,
-                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2)
+                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
@@ -117,15 +117,18 @@ def cgroup_for(c0, c1=0):
 
 def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, dst0, n0=None,
           src1=None, c1=0, bias=None, dst1=None, mask0=None, mask1=None, relu=False, accum=False,
-          shuffle=False, cgroup=0):
-    """pu_conv_igemm: implicit-GEMM conv (3x3 fwd/dgrad, ConvT fwd with shuffle, ConvT dgrad)."""
+          shuffle=False, cgroup=0, resid=None, shuf=(0, 0, 0)):
+    """pu_conv_igemm: implicit-GEMM conv (3x3 fwd/dgrad, ConvT fwd with shuffle, ConvT dgrad).
+    resid: residual tensor added before ReLU/mask; shuf = (out_h, out_w, crop) of a SHUFFLE2 grid."""
     for t, nm in ((src0, "src0"), (src1, "src1"), (weight, "weight"), (bias, "bias"), (dst0, "dst0"),
-                  (dst1, "dst1"), (mask0, "mask0"), (mask1, "mask1")):
+                  (dst1, "dst1"), (mask0, "mask0"), (mask1, "mask1"), (resid, "resid")):
         _req(t, nm)
-    flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0)
+    flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
+        | (PU_EPI_RESID if resid is not None else 0)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
-                 _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0)
+                 _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,
+                 _p(resid), shuf[0], shuf[1], shuf[2])
     L = lib()
     nbytes = L.pu_conv_igemm_workspace_bytes(ctypes.byref(a))
     if nbytes:     # split-K scratch from the caching allocator (stream-ordered reuse)
@@ -173,7 +176,7 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0):
     _req(w, "w")
     d0, d1, kh, kw = w.shape
     taps = kh * kw
-    rows = {0: d0, 1: d1, 2: taps * d1, 3: d0}[mode]
+    rows = {0: d0, 1: d1, 2: taps * d1, 3: d0, 4: 4 * d1}[mode]
     if out is None:
         out = torch.empty(rows, k_pad, dtype=torch.float32, device=w.device)
     with _Rec("pack_weight", nbytes=4.0 * (w.numel() + out.numel())):
@@ -187,6 +190,32 @@ def nchw_to_nhwc(x):
     B, C, H, W = x.shape
     out = torch.empty(B, H, W, C, dtype=torch.float32, device=x.device)
     check(lib().pu_nchw_to_nhwc(x.data_ptr(), out.data_ptr(), B, C, H, W, _stream()), "pu_nchw_to_nhwc")
+    return out
+
+
+def channel_scale(x, scale, out=None):
+    """Dropout2d on NHWC x [B,H,W,C] with per-(sample, channel) scale [B,C]; out may be x."""
+    _req(x, "x"); _req(scale, "scale")
+    B, H, W, C = x.shape
+    y = torch.empty_like(x) if out is None else out
+    with _Rec("channel_scale", nbytes=8.0 * x.numel()):
+        check(lib().pu_channel_scale(x.data_ptr(), scale.data_ptr(), y.data_ptr(), B, H * W, C, _stream()),
+              "pu_channel_scale")
+    return y
+
+
+def column_sum(x2d, out=None, accumulate=False):
+    """Deterministic fp64 column sums of a row-major [rows, cols] tensor."""
+    _req(x2d, "x")
+    rows, cols = x2d.shape
+    if out is None:
+        out = torch.empty(cols, dtype=torch.float32, device=x2d.device)
+    L = lib()
+    nbytes = L.pu_column_sum_workspace_bytes(rows, cols)
+    ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=x2d.device)
+    with _Rec("column_sum", nbytes=4.0 * x2d.numel()):
+        check(L.pu_column_sum(x2d.data_ptr(), rows, cols, out.data_ptr(), int(accumulate), ws.data_ptr(), nbytes,
+                              _stream()), "pu_column_sum")
     return out
 
 

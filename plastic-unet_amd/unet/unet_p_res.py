@@ -1,9 +1,10 @@
 """UNetpRes - drop-in for yaricom/Plastic-UNet ``src/unet/unet_p_res.py`` (module tree / state_dict
 compatible; constructor signature and defaults unchanged).
 
-The residual trunk's MI355X kernels (residual-add epilogue, ConvTranspose2d 3x3 s2 + crop,
-Dropout2d) are the next row of SURVEY.md section 8; until they land, forward() raises instead of
-silently falling back to ATen.
+forward() runs the residual trunk as HIP kernels (punet.res_trunk: residual-add conv epilogues,
+ConvTranspose2d 3x3 s2 with the row/col-0 crop, Dropout2d channel masks in training mode) and the
+plastic head of unet_p_res.py:115-134 (punet.head).  Like UNetp it batches B per-slot traces when
+hebb is [B,nbf,nbf]; there is no CPU path.
 """
 import torch
 import torch.nn as nn
@@ -101,9 +102,50 @@ class UNetpRes(nn.Module):
         self.to(device)
         print("UNet plastic model with plastic rule [%s] initialized" % self.rule)
 
+    def _trunk_plan(self):
+        if getattr(self, "_trunk", None) is None:
+            from punet.res_trunk import ResTrunk
+            self._trunk = ResTrunk(self)
+        return self._trunk
+
     def forward(self, x, hebb):
-        raise NotImplementedError("UNetpRes on the MI355X path is the next build item (SURVEY.md 8f); "
-                                  "use UNetp (the C1-C3 configurations)")
+        from .unet_p import _check_gpu_tensor
+        single = hebb.dim() == 2
+        B, C, Hh, Ww = x.shape
+        if single and B != 1:
+            # the reference has no explicit check: activin = x.view(nbf, nbf) fails (S8)
+            raise RuntimeError("shape '[%d, %d]' is invalid for input of size %d"
+                               % (self.nbf, self.nbf, B * Hh * Ww * self.n_classes))
+        if self.alfa_type not in ("free", "yoked"):
+            raise ValueError("Must select one plasticity coefficient type ('free' or 'yoked')")
+        if self.rule not in ("hebb", "oja"):
+            raise ValueError("Must select one learning rule ('hebb' or 'oja')")
+        _check_gpu_tensor(x, "x")
+        _check_gpu_tensor(hebb, "hebb")
+        if self.n_classes != 1:
+            raise RuntimeError("the plastic head needs n_classes == 1 (activin = x.view(nbf, nbf))")
+        if C != self.n_channels:
+            raise RuntimeError("expected input with %d channels, got %d" % (self.n_channels, C))
+        if Hh * Ww != self.nbf * self.nbf or Hh != Ww:
+            raise RuntimeError("shape '[%d, %d]' is invalid for input of size %d" % (self.nbf, self.nbf, Hh * Ww))
+        if Hh < 16:
+            raise RuntimeError("UNetpRes needs images of at least 16x16 (four 2x2 poolings)")
+        H = hebb.unsqueeze(0) if single else hebb
+        if H.shape != (B, self.nbf, self.nbf):
+            raise ValueError("hebb must be [nbf,nbf] or [B,nbf,nbf]; got %s for batch %d" % (tuple(hebb.shape), B))
+        if x.dtype != torch.float32:
+            x = x.float()
+        from punet.res_trunk import ResTrunkFunction
+        from punet.head import PlasticHeadFunction, RULES
+        trunk = self._trunk_plan()
+        params = trunk.params
+        save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        logits = ResTrunkFunction.apply(trunk, save, self.training, x, *params)
+        sink = None if trunk.gradbuf is None else (trunk.gradbuf, self.w, self.alpha)
+        Y, Hn = PlasticHeadFunction.apply(logits, H, self.w, self.alpha, self.eta, RULES[self.rule], True, sink)
+        if single:
+            return Y[0], Hn[0]
+        return Y, Hn
 
     def initialZeroHebb(self, batch=None):
         shape = (self.nbf, self.nbf) if batch is None else (batch, self.nbf, self.nbf)
