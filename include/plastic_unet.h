@@ -172,6 +172,12 @@ int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w
 int pu_channel_scale(const float* x, const float* scale, float* y, int batch, long long hw, int c,
                      void* stream);
 
+/* AddCoords (coord_conv_script.py:69-96) fused with the NCHW -> NHWC input transpose:
+ * out[b][i][j] = (x[b][0..c)[i][j], xx_j, yy_i [, rr_ij]) with xx_j = 2j/(h-1) - 1,
+ * yy_i = 2i/(w-1) - 1 (the script's x_dim/y_dim roles; square images), rr = sqrt((xx-.5)^2+(yy-.5)^2).
+ * out has c + 2 + with_r channels. */
+int pu_add_coords(const float* x, float* out, int batch, int c, int h, int w, int with_r, void* stream);
+
 /* Column sums of a row-major [rows][cols] matrix in fp64, fixed order (deterministic):
  * out[c] (+)= sum_r x[r][c].  (ConvTranspose2d 3x3 bias gradient.) */
 size_t pu_column_sum_workspace_bytes(long long rows, int cols);

@@ -298,6 +298,37 @@ __global__ void channel_scale_kernel(const float* __restrict__ x, const float* _
     }
 }
 
+// AddCoords + NCHW->NHWC: one thread per output element (channel fastest); fp32 with no
+// contraction so the coordinate values are those of the elementwise CPU ops
+#pragma clang fp contract(off)
+__global__ void add_coords_kernel(const float* __restrict__ x, float* __restrict__ out, int c, int h, int w,
+                                  int with_r, long long total) {
+    const int co = c + 2 + with_r;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const long long pix = idx / co;
+        const int ch = int(idx - pix * co);
+        const long long hw = (long long)h * w;
+        const long long b = pix / hw;
+        const int rem = int(pix - b * hw);
+        const int i = rem / w, j = rem - (rem / w) * w;
+        float v;
+        if (ch < c) {
+            v = x[(b * c + ch) * hw + rem];
+        } else {
+            const float xx = ((float)j / (float)(h - 1)) * 2.0f - 1.0f;
+            const float yy = ((float)i / (float)(w - 1)) * 2.0f - 1.0f;
+            if (ch == c) v = xx;
+            else if (ch == c + 1) v = yy;
+            else {
+                const float dx = xx - 0.5f, dy = yy - 0.5f;
+                v = sqrtf(dx * dx + dy * dy);
+            }
+        }
+        out[idx] = v;
+    }
+}
+
 // column sums, pass 1: block q sums rows [q*rpb, (q+1)*rpb) of column chunk blockIdx.y (256 cols)
 // in fp64; threads = (row lane, column) with rl = 256 / cw row lanes
 __global__ void colsum_partial_kernel(const float* __restrict__ x, long long rows, int cols, long long rpb,
@@ -477,4 +508,13 @@ extern "C" int pu_column_sum(const float* x, long long rows, int cols, float* ou
     hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, as_stream(stream), part, nb, cols,
                        out, accumulate);
     return check_launch("pu_column_sum");
+}
+
+extern "C" int pu_add_coords(const float* x, float* out, int batch, int c, int h, int w, int with_r, void* stream) {
+    PU_REQUIRE(x && out && batch > 0 && c > 0 && h > 1 && w > 1 && (with_r == 0 || with_r == 1),
+               "pu_add_coords: bad args");
+    const long long total = (long long)batch * h * w * (c + 2 + with_r);
+    hipLaunchKernelGGL(add_coords_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, out, c, h, w,
+                       with_r, total);
+    return check_launch("pu_add_coords");
 }

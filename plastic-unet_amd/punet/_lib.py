@@ -70,6 +70,7 @@ SIGNATURES = [
     ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_nchw_to_nhwc", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_channel_scale", c_int, [P, P, P, c_int, c_ll, c_int, P]),
+    ("pu_add_coords", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_column_sum_workspace_bytes", c_size, [c_ll, c_int]),
     ("pu_column_sum", c_int, [P, c_ll, c_int, P, c_int, P, c_size, P]),
     ("pu_maxpool2_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),

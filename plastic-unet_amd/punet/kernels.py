@@ -204,6 +204,16 @@ def channel_scale(x, scale, out=None):
     return y
 
 
+def add_coords(x, with_r):
+    """NCHW input [B,C,H,W] -> NHWC [B,H,W,C+2(+1)] with the AddCoords channels appended."""
+    _req(x, "x")
+    B, C, H, W = x.shape
+    out = torch.empty(B, H, W, C + 2 + int(with_r), dtype=torch.float32, device=x.device)
+    with _Rec("add_coords", nbytes=4.0 * (x.numel() + out.numel())):
+        check(lib().pu_add_coords(x.data_ptr(), out.data_ptr(), B, C, H, W, int(with_r), _stream()), "pu_add_coords")
+    return out
+
+
 def column_sum(x2d, out=None, accumulate=False):
     """Deterministic fp64 column sums of a row-major [rows, cols] tensor."""
     _req(x2d, "x")

@@ -10,6 +10,9 @@ Forward (NHWC, fp32), per stage:
   up_j    : ConvT2x2s2 (GEMM + pixel-shuffle epilogue) -> conv3x3+ReLU over [skip | upsampled]
             read from two buffers (no concat copy) -> conv3x3+ReLU
   outc    : 1x1 conv C -> 1 (logits)
+The CoordConv U-Net of src/coord_conv_script.py:146-200 (config C4) is the same schedule with a
+stem - AddCoords fused into the input transpose (pu_add_coords) + 1x1 conv + ReLU - and Keras-style
+up stages: ConvT2x2s2 halving the channels and the concat [upsampled | skip] (upsampled FIRST).
 Backward fuses every ReLU mask into the producing kernel's epilogue (dgrad / maxpool-bwd /
 outconv-bwd multiply by (activation > 0)), writes skip gradients once and lets the max-pool
 backward accumulate into them, and gets bias gradients from the weight-gradient GEMM (a ones
@@ -129,10 +132,14 @@ def as_nhwc_input(x):
 
 
 class UNetpTrunk:
-    """Parameter order and kernel schedule of the generalised UNetp trunk (depth D)."""
+    """Parameter order and kernel schedule of the generalised UNetp trunk (depth D).  Models with a
+    ``coord`` stem (CoordConvUNetp) get its w,b appended after outc and ``up_first`` concats."""
 
     def __init__(self, model):
         self.depth = model.depth
+        self.coord = getattr(model, "coord", None)
+        self.with_r = bool(getattr(model, "with_r", False))
+        self.up_first = bool(getattr(model, "up_first", False))
         self.names = []
         self.packs = _Packs()
         mods = {"inc": model.inc.conv.conv}
@@ -155,6 +162,8 @@ class UNetpTrunk:
             for idx in (0, 2):
                 self.params += [seq[idx].weight, seq[idx].bias]
         self.params += [model.outc.conv.weight, model.outc.conv.bias]
+        if self.coord is not None:
+            self.params += [self.coord.conv.weight, self.coord.conv.bias]
         self.gradbuf = None      # punet.dp.GradBuffer: backward writes grads into its views
         self.debug = None        # dict: when set, backward stores each layer's dZ (tests/diagnostics)
 
@@ -174,6 +183,14 @@ class UNetpTrunk:
         D = self.depth
         pk = self.packs
         s = {"x": x}
+        if self.coord is not None:     # stem: 1x1 conv + ReLU over the AddCoords input
+            cw, cb = params[-2], params[-1]
+            B, H, W, ca = x.shape
+            x = torch.empty(B, H, W, cw.shape[0], dtype=torch.float32, device=cw.device)
+            K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, src0=s["x"], c0=ca,
+                    weight=pk.get(cw, PU_PACK_CONV_FWD, K.round16(ca)), k_pad=K.round16(ca), n=cw.shape[0],
+                    bias=cb, dst0=x, relu=True)
+            s["stem"] = x
         w, b = nxt(); t = conv3x3(x, w, b, pk); s["inc.t"] = t
         w, b = nxt(); y = conv3x3(t, w, b, pk)
         skips = [y]
@@ -187,7 +204,11 @@ class UNetpTrunk:
         for j in range(1, D):
             skip = skips[D - 1 - j]
             w, b = nxt(); u = convT2x2(y, w, b, pk); s["up%d.u" % j] = u
-            w, b = nxt(); t = conv3x3(skip, w, b, pk, x1=u); s["up%d.t" % j] = t
+            if self.up_first:
+                w, b = nxt(); t = conv3x3(u, w, b, pk, x1=skip)
+            else:
+                w, b = nxt(); t = conv3x3(skip, w, b, pk, x1=u)
+            s["up%d.t" % j] = t
             w, b = nxt(); y = conv3x3(t, w, b, pk)
             s["up%d.y" % j] = y
         w, b = nxt()
@@ -227,10 +248,13 @@ class UNetpTrunk:
             # conv1 of up_j: y_j = relu(conv(t));  g = dZ
             grads[base + 4], grads[base + 5] = conv3x3_wgrad(g, t, out=out(base + 4))
             dt, _ = conv3x3_dgrad(g, P[base + 4], pk, mask0=t)
-            # conv0 over [skip | u]
-            grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, skip, u, out=out(base + 2))
-            cs = skip.shape[3]
-            dskip, du = conv3x3_dgrad(dt, P[base + 2], pk, split=cs, mask0=skip)
+            # conv0 over [skip | u]  (up_first: [u | skip])
+            if self.up_first:
+                grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, u, skip, out=out(base + 2))
+                du, dskip = conv3x3_dgrad(dt, P[base + 2], pk, split=u.shape[3], mask1=skip)
+            else:
+                grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, skip, u, out=out(base + 2))
+                dskip, du = conv3x3_dgrad(dt, P[base + 2], pk, split=skip.shape[3], mask0=skip)
             if self.debug is not None:
                 self.debug["up%d.c0" % j] = dt
                 self.debug["up%d.up" % j] = du
@@ -258,9 +282,20 @@ class UNetpTrunk:
             self.debug["inc.c1"] = g
         grads[2], grads[3] = conv3x3_wgrad(g, t, out=out(2))
         dt, _ = conv3x3_dgrad(g, P[2], pk, mask0=t)
-        grads[0], grads[1] = conv3x3_wgrad(dt, s["x"], out=out(0))
+        x0 = s["stem"] if self.coord is not None else s["x"]
+        grads[0], grads[1] = conv3x3_wgrad(dt, x0, out=out(0))
         if self.debug is not None:
             self.debug["inc.c0"] = dt
+        if self.coord is not None:     # stem 1x1 conv: dgrad of inc.c0 (masked by the stem ReLU) + wgrad
+            dstem, _ = conv3x3_dgrad(dt, P[0], pk, mask0=x0)
+            B, H, W, ca = s["x"].shape
+            cs = len(P) - 2
+            o = out(cs)
+            dw = torch.empty(P[cs].shape, dtype=torch.float32, device=dt.device) if o is None else o[0]
+            db = torch.empty(P[cs + 1].shape, dtype=torch.float32, device=dt.device) if o is None else o[1]
+            K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, rows=dstem, n=P[cs].shape[0],
+                    src0=s["x"], c0=ca, bias_mode=1, dweight=dw, dbias=db)
+            grads[cs], grads[cs + 1] = dw, db
         return grads
 
 
@@ -270,7 +305,10 @@ class TrunkFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, trunk, save, x, *params):
         # ``save`` is decided by the caller: grad mode is always off inside Function.forward
-        xin = as_nhwc_input(x.detach())
+        if trunk.coord is not None:
+            xin = K.add_coords(x.detach().contiguous(), trunk.with_r)
+        else:
+            xin = as_nhwc_input(x.detach())
         detached = [p.detach() for p in params]
         logits, saved = trunk.forward(xin, detached, save)
         ctx.trunk = trunk
