@@ -5,7 +5,9 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Workload = config C2 (BASELINE.json configs[1]): UNetp depth 5 / base 64 (14.81 M params), Oja
-rule, 1x128x128 synthetic tiles, batch 32 per GPU, fp32.  A step = forward + BCE + backward
+rule, 1x128x128 synthetic tiles, batch 32 per GPU, fp32.  --config c4 / c5 measure the other
+single-GPU configurations (CoordConv U-Net 256x256 bs 32; UNetpRes neurons 8 512x512 bs 16 per GPU
+with Dropout2d active) - parity/coverage lines, not the headline.  A step = forward + BCE + backward
 (+ RCCL gradient all-reduce when N > 1) + Adam + StepLR over one resident batch, with the per-slot
 plastic traces carried step to step.  Timed region: barrier + synchronize on both sides, max over
 ranks; value = images of all ranks / time (weak scaling: 32 images per GPU).
@@ -36,10 +38,11 @@ import torch.distributed as dist  # noqa: E402
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
-    ap.add_argument("--img", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (c2/c4: 32, c5: 16)")
+    ap.add_argument("--img", type=int, default=None, help="image side (c2: 128, c4: 256, c5: 512)")
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--base", type=int, default=64)
     ap.add_argument("--rule", default="oja")
@@ -49,7 +52,38 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-profile", action="store_true")
     ap.add_argument("--no-oja", action="store_true", help="skip the Oja-update HBM benchmark")
-    return ap.parse_args()
+    a = ap.parse_args()
+    dflt = {"c2": (32, 128), "c4": (32, 256), "c5": (16, 512)}[a.config]
+    a.batch = a.batch or dflt[0]
+    a.img = a.img or dflt[1]
+    return a
+
+
+CONFIGS = {
+    "c2": "C2: UNetp depth %(depth)d base_ch %(base)d, %(rule)s rule, 1x%(img)dx%(img)d, fwd+BCE+bwd+Adam",
+    "c4": "C4: CoordConv-UNet (coord_conv_script.py topology, with_r) base 8 depth 5 + plastic head, %(rule)s rule, "
+          "1x%(img)dx%(img)d, fwd+BCE+bwd+Adam",
+    "c5": "C5: UNetpRes neurons 8, Dropout2d 0.5 (train mode), %(rule)s rule, 1x%(img)dx%(img)d, fwd+BCE+bwd+Adam",
+}
+
+
+def build_model(args, device, ref=False):
+    """The configuration's model: the MI355X product class, or (ref=True) the CPU oracle's."""
+    if ref:
+        import oracle
+        if args.config == "c4":
+            return oracle.RefCoordConvUNetp(1, 1, rule=args.rule, nbf=args.img, base_ch=8, with_r=True, depth=5)
+        if args.config == "c5":
+            return oracle.RefUNetpRes(1, 1, neurons=8, rule=args.rule, nbf=args.img)
+        return oracle.RefUNetp(1, 1, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base)
+    if args.config == "c4":
+        from unet import CoordConvUNetp
+        return CoordConvUNetp(1, 1, device, rule=args.rule, nbf=args.img, base_ch=8, with_r=True, depth=5)
+    if args.config == "c5":
+        from unet import UNetpRes
+        return UNetpRes(1, 1, device, neurons=8, rule=args.rule, nbf=args.img)
+    from unet import UNetp
+    return UNetp(1, 1, device, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base)
 
 
 def fp32_mfma_peak_tflops(kernels):
@@ -66,7 +100,8 @@ def cpu_baseline(args):
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
     torch.manual_seed(0)
-    net = oracle.RefUNetp(1, 1, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base)
+    net = build_model(args, None, ref=True)
+    net.train()
     opt = oracle.ref_adam(net.parameters(), args.lr)
     sch = oracle.ref_steplr(opt, int(args.steplr))
     g = torch.Generator().manual_seed(4321)
@@ -82,16 +117,17 @@ def cpu_baseline(args):
         if (el >= args.cpu_seconds and n >= 2) or n >= 200:
             break
     return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": "oracle/ref_cpu.py RefUNetp depth %d base %d %dx%d, reference mode (bs=1, fwd+BCE+bwd+Adam "
-                      "per sample, train.py:91-112): %d samples in %.1f s on %d threads"
-                      % (args.depth, args.base, args.img, args.img, n, el, threads)}
+            "sample": "oracle/ref_cpu.py %s %dx%d, reference mode (bs=1, fwd+BCE+bwd+Adam per sample, "
+                      "train.py:91-112): %d samples in %.1f s on %d threads"
+                      % (type(net).__name__, args.img, args.img, n, el, threads)}
 
 
 def oja_update_bench(K, B, N, device):
     """Algorithmic GB/s of the trace update: 8*B*N^2 + 8*B*N bytes (read H, write H', rows)."""
     res = {}
     eta = torch.full((1,), 0.01, device=device)
-    for label, bb, reps in (("bs%d" % B, B, 200), ("hbm_sweep_8192", 8192, 20)):
+    sweep = max(1, (1 << 30) // (4 * N * N))            # 1 GiB of traces (8192 at N=128)
+    for label, bb, reps in (("bs%d" % B, B, 200), ("hbm_sweep_%d" % sweep, sweep, 20)):
         H = torch.randn(bb, N, N, device=device)
         X = torch.randn(bb, N, N, device=device)
         Y = torch.rand(bb, N, N, device=device)
@@ -121,12 +157,12 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
 
-    from unet import UNetp
     from punet import kernels as K
     from punet.engine import Trainer
 
     torch.manual_seed(0)
-    net = UNetp(1, 1, device, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base)
+    net = build_model(args, device)
+    net.train()
     dp.broadcast_params(net)
     trainer = Trainer(net, lr=args.lr, steplr=args.steplr)
 
@@ -213,7 +249,7 @@ def main():
     if rank == 0:
         value = world * B * args.steps / elapsed
         line = {
-            "metric": "training images/sec (128x128, bs=32 per GPU)",
+            "metric": "training images/sec (%dx%d, bs=%d per GPU)" % (S, S, B),
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -225,8 +261,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: x~U[0,1) [B,1,%d,%d], targets (U>0.5); random init (seed 0)" % (S, S),
-            "config": {"workload": "C2: UNetp depth %d base_ch %d, %s rule, 1x%dx%d, fwd+BCE+bwd+Adam"
-                                   % (args.depth, args.base, args.rule, S, S),
+            "config": {"workload": CONFIGS[args.config] % vars(args),
                        "global_batch": world * B, "per_gpu_batch": B, "img": S,
                        "parallelism": "dp%d" % world if world > 1 else "single"},
             "final_loss": final_loss,
