@@ -329,37 +329,81 @@ __global__ void add_coords_kernel(const float* __restrict__ x, float* __restrict
     }
 }
 
-// column sums, pass 1: block q sums rows [q*rpb, (q+1)*rpb) of column chunk blockIdx.y (256 cols)
-// in fp64; threads = (row lane, column) with rl = 256 / cw row lanes
+// column sums, pass 1: block q sums rows [q*rpb, (q+1)*rpb) of column chunk blockIdx.y in fp64.
+// cols % 4 == 0: threads = (row lane, float4 column group) over a 1024-column chunk, 4 rows in
+// flight per thread (independent accumulators, fixed combine order); else scalar columns.
+template <bool VEC>
 __global__ void colsum_partial_kernel(const float* __restrict__ x, long long rows, int cols, long long rpb,
                                       double* __restrict__ part) {
-    __shared__ double red[256];
-    const int c0 = blockIdx.y * 256;
-    const int cw = min(256, cols - c0);
+    __shared__ double red[256 * 4];
+    constexpr int W = VEC ? 4 : 1;
+    const int c0 = blockIdx.y * 256 * W;
+    const int cw = min(256, (cols - c0 + W - 1) / W);     // column groups in this chunk
     const int rl = 256 / cw;
     const int t = threadIdx.x;
-    const int col = t % cw, lane = t / cw;
-    double s = 0.0;
+    const int cg = t % cw, lane = t / cw;
+    double s[4][W];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < W; ++k) s[u][k] = 0.0;
     const long long r0 = blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-    if (lane < rl)
-        for (long long r = r0 + lane; r < r1; r += rl) s += (double)x[r * cols + c0 + col];
-    red[t] = s;
+    if (lane < rl) {
+        const int col = c0 + cg * W;
+        long long r = r0 + lane;
+        for (; r + 3LL * rl < r1; r += 4LL * rl) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float* src = x + (r + (long long)u * rl) * cols + col;
+                if (VEC) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+                    for (int k = 0; k < W; ++k) s[u][k] += (double)v[k];
+                } else {
+                    s[u][0] += (double)src[0];
+                }
+            }
+        }
+        for (; r < r1; r += rl) {
+            const float* src = x + r * cols + col;
+            if (VEC) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+                for (int k = 0; k < W; ++k) s[0][k] += (double)v[k];
+            } else {
+                s[0][0] += (double)src[0];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < W; ++k) red[t * W + k] = (s[0][k] + s[1][k]) + (s[2][k] + s[3][k]);
     __syncthreads();
     if (t < cw) {
-        double v = 0.0;
-        for (int l = 0; l < rl; ++l) v += red[l * cw + t];
-        part[(long long)blockIdx.x * cols + c0 + t] = v;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            double v = 0.0;
+            for (int l = 0; l < rl; ++l) v += red[(l * cw + t) * W + k];
+            const int col = c0 + t * W + k;
+            if (col < cols) part[(long long)blockIdx.x * cols + col] = v;
+        }
     }
 }
 
-// pass 2: out[c] (+)= sum over the partial blocks in order
+// pass 2: out[c] (+)= sum over the partial blocks, one block per column: strided fp64 partial
+// sums in a fixed thread order, then a fixed LDS tree (deterministic)
 __global__ void colsum_final_kernel(const double* __restrict__ part, int nparts, int cols, float* __restrict__ out,
                                     int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= cols) return;
+    __shared__ double red[256];
+    const int c = blockIdx.x;
     double s = 0.0;
-    for (int q = 0; q < nparts; ++q) s += part[(long long)q * cols + c];
-    out[c] = accumulate ? out[c] + (float)s : (float)s;
+    for (int q = threadIdx.x; q < nparts; q += 256) s += part[(long long)q * cols + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)red[0] : (float)red[0];
 }
 
 static int colsum_blocks(long long rows) {
@@ -503,10 +547,14 @@ extern "C" int pu_column_sum(const float* x, long long rows, int cols, float* ou
     const int nb = colsum_blocks(rows);
     const long long rpb = (rows + nb - 1) / nb;
     double* part = (double*)workspace;
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nb, (cols + 255) / 256), dim3(256), 0, as_stream(stream), x, rows,
-                       cols, rpb, part);
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, as_stream(stream), part, nb, cols,
-                       out, accumulate);
+    if (cols % 4 == 0 && ((uintptr_t)x & 15) == 0)
+        hipLaunchKernelGGL(colsum_partial_kernel<true>, dim3(nb, (cols + 1023) / 1024), dim3(256), 0,
+                           as_stream(stream), x, rows, cols, rpb, part);
+    else
+        hipLaunchKernelGGL(colsum_partial_kernel<false>, dim3(nb, (cols + 255) / 256), dim3(256), 0,
+                           as_stream(stream), x, rows, cols, rpb, part);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(cols), dim3(256), 0, as_stream(stream), part, nb, cols, out,
+                       accumulate);
     return check_launch("pu_column_sum");
 }
 

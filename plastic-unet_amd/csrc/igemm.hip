@@ -576,6 +576,116 @@ __global__ __launch_bounds__(256) void igemm_splitk_epilogue_kernel(const IgemmP
     epi_store4(p, epi_row(p, m), n, v);
 }
 
+// ---------------------------------------------------------------- small-channel direct conv
+// For 3x3/s1/p1 convolutions with C <= 16 input and N <= 16 output channels (the 8/16-channel
+// levels of configs C4/C5) a GEMM tile is mostly padding: N = 8 fills 1/8 of a 64-wide MFMA
+// tile and K = 72 leaves the per-block setup dominant.  These layers are HBM-bound (~18-36
+// FLOP/B), so they run as a direct convolution on the VALU: a block stages the (16+2) x (32+2)
+// input halo of a 16 x 32 output tile in LDS (both concat sources, zero padding), each thread
+// computes 2 adjacent pixels x all N channels with fmaf chains over (tap, channel) - the same
+// k order as the MFMA path - reading the packed weight rows with wave-uniform (scalar) loads, and
+// the float4 epilogue above applies bias / residual / ReLU / mask / split / accumulate.
+constexpr int SC_TH = 16, SC_TW = 32;
+
+template <int C, int N>
+__global__ __launch_bounds__(256) void smallconv_kernel(const IgemmParams p) {
+    constexpr int HH = SC_TH + 2, HWD = SC_TW + 2;
+    constexpr int CP = (C + 3) & ~3;     // LDS channel stride (float4 reads when C % 4 == 0)
+    __shared__ __attribute__((aligned(16))) float tile[HH * HWD * CP];
+    const int tiles_w = (p.Wo + SC_TW - 1) / SC_TW;
+    const int tiles_h = (p.Ho + SC_TH - 1) / SC_TH;
+    int blk = blockIdx.x;
+    const int txi = blk % tiles_w;
+    blk /= tiles_w;
+    const int tyi = blk % tiles_h;
+    const int b = blk / tiles_h;
+    const int y0 = tyi * SC_TH - 1, x0 = txi * SC_TW - 1;   // halo origin (pad 1)
+    const long long img = (long long)b * p.Hi * p.Wi;
+
+    // stage the halo: element (hy, hx, c) from src0 (c < c0) or src1
+    if (C % 4 == 0 && p.c0 % 4 == 0) {
+        constexpr int Q = C / 4;
+        for (int e = threadIdx.x; e < HH * HWD * Q; e += 256) {
+            const int q = e % Q, pix = e / Q;
+            const int hx = pix % HWD, hy = pix / HWD;
+            const int gy = y0 + hy, gx = x0 + hx;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
+                const long long px = img + (long long)gy * p.Wi + gx;
+                const int c = 4 * q;
+                v = c < p.c0 ? *reinterpret_cast<const f32x4*>(p.src0 + px * p.c0 + c)
+                             : *reinterpret_cast<const f32x4*>(p.src1 + px * p.c1 + (c - p.c0));
+            }
+            *reinterpret_cast<f32x4*>(tile + pix * CP + 4 * q) = v;
+        }
+    } else {
+        for (int e = threadIdx.x; e < HH * HWD * CP; e += 256) {
+            const int c = e % CP, pix = e / CP;
+            const int hx = pix % HWD, hy = pix / HWD;
+            const int gy = y0 + hy, gx = x0 + hx;
+            float v = 0.f;
+            if (c < C && (unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
+                const long long px = img + (long long)gy * p.Wi + gx;
+                v = c < p.c0 ? p.src0[px * p.c0 + c] : p.src1[px * p.c1 + (c - p.c0)];
+            }
+            tile[pix * CP + c] = v;
+        }
+    }
+    __syncthreads();
+
+    const int row = threadIdx.x / (SC_TW / 2);
+    const int col = (threadIdx.x % (SC_TW / 2)) * 2;
+    float acc0[N], acc1[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) { acc0[n] = 0.f; acc1[n] = 0.f; }
+    // one (tap, 4-channel) step per iteration, not unrolled: only its 4*N weights are live
+    // (scalar registers, used directly as FMA operands)
+    constexpr int Q4 = CP / 4;
+#pragma unroll 1
+    for (int step = 0; step < 9 * Q4; ++step) {
+        const int tap = step / Q4, c4 = (step - tap * Q4) * 4;
+        const int r = tap / 3, sx = tap - r * 3;
+        const float* t0 = tile + ((row + r) * HWD + col + sx) * CP + c4;
+        const float* wt = p.wt + tap * C + c4;            // + n * k_pad: wave-uniform
+        // (packed v_pk_fma_f32 measured no faster: these layers are HBM-bound)
+        float a0[4], a1[4];
+        if (C % 4 == 0) {
+            const f32x4 v0 = *reinterpret_cast<const f32x4*>(t0);
+            const f32x4 v1 = *reinterpret_cast<const f32x4*>(t0 + CP);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { a0[e] = v0[e]; a1[e] = v1[e]; }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { a0[e] = t0[e]; a1[e] = t0[CP + e]; }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (e >= C) break;
+#pragma unroll
+            for (int n = 0; n < N; ++n) {
+                const float w = wt[(long long)n * p.k_pad + e];
+                acc0[n] = fmaf(a0[e], w, acc0[n]);
+                acc1[n] = fmaf(a1[e], w, acc1[n]);
+            }
+        }
+    }
+    const int oy = tyi * SC_TH + row, ox = txi * SC_TW + col;
+    if (oy >= p.Ho) return;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        if (ox + q >= p.Wo) break;
+        const int m = (b * p.Ho + oy) * p.Wo + ox + q;
+        const EpiRow er = epi_row(p, m);
+#pragma unroll
+        for (int n = 0; n < N; n += 4) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = q ? acc1[n + e] : acc0[n + e];
+            epi_store4(p, er, n, v);
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------ host
 struct TileCfg {
     int bm, bn;
@@ -644,6 +754,21 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
     *ksplit = ceil_div(T, *t_per);
 }
 
+// the small-channel direct convolution handles: 3x3 / s1 / p1 (same size), C in {1,4,8,12,16},
+// N in {4,8,16}, tap-major weight rows, float4 epilogue
+#ifndef PU_NO_SMALLCONV
+#define PU_NO_SMALLCONV 0
+#endif
+static bool small_conv_ok(const pu_conv_args* a) {
+    const int C = a->c0 + a->c1;
+    const bool cset = C == 1 || C == 4 || C == 8 || C == 12 || C == 16;
+    const bool nset = a->n == 4 || a->n == 8 || a->n == 16;
+    const bool nc = (a->n == 4) ? (C == 4 || C == 8 || C == 16) : true;
+    return !PU_NO_SMALLCONV && cset && nset && nc && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
+           a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) && vec_epilogue(a) &&
+           (a->cgroup == 0 || a->cgroup >= C) && (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
+}
+
 static size_t split_bytes(long long M, int n, int ksplit) {
     return ksplit > 1 ? (size_t)ksplit * (size_t)M * (size_t)n * sizeof(float) : 0;
 }
@@ -709,6 +834,16 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
 
     hipStream_t s = as_stream(stream);
     const int N = a->n;
+    if (small_conv_ok(a)) {
+        p.ksplit = 1;
+        const dim3 sgrid((unsigned)(((a->out_w + SC_TW - 1) / SC_TW) * ((a->out_h + SC_TH - 1) / SC_TH) * a->batch));
+#define PU_SC(C_, N_) if (C == C_ && N == N_) hipLaunchKernelGGL((smallconv_kernel<C_, N_>), sgrid, dim3(256), 0, s, p)
+        PU_SC(1, 8); else PU_SC(1, 16); else PU_SC(4, 8); else PU_SC(4, 16); else PU_SC(8, 8); else PU_SC(8, 16);
+        else PU_SC(12, 8); else PU_SC(12, 16); else PU_SC(16, 8); else PU_SC(16, 16);
+        else PU_SC(4, 4); else PU_SC(8, 4); else PU_SC(16, 4);
+#undef PU_SC
+        return check_launch("pu_conv_igemm (small-channel)");
+    }
     int bm, bn;
     choose_tile(M, N, &bm, &bn);
     p.gn = ceil_div(N, bn);
@@ -738,6 +873,7 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
 extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
     if (!a || a->batch <= 0 || a->out_h <= 0 || a->out_w <= 0 || a->n <= 0 || a->k_pad <= 0) return 0;
     const long long M = (long long)a->batch * a->out_h * a->out_w;
+    if (small_conv_ok(a)) return 0;
     int bm, bn, ks, tp;
     choose_tile(M, a->n, &bm, &bn);
     plan_split(a, M, bm, bn, &ks, &tp);
@@ -749,6 +885,13 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
     const long long M = (long long)a->batch * a->out_h * a->out_w;
     choose_tile(M, a->n, bm, bn);
     *mode = choose_mode(a->c0, a->c1);
+    if (small_conv_ok(a)) {          // reported as mode 3 ("direct"), tile SC_TH x SC_TW pixels
+        *bm = SC_TH * SC_TW;
+        *bn = a->n;
+        *mode = 3;
+        if (ksplit) *ksplit = 1;
+        return PU_OK;
+    }
     if (ksplit) {
         int ks, tp;
         plan_split(a, M, *bm, *bn, &ks, &tp);

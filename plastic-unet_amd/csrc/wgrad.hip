@@ -31,6 +31,7 @@ struct WgradParams {
     int mps;  // pixel rows per split (multiple of WG_BM)
     int gx, gy;  // k-tiles, n-tiles
     int Kcp;     // slab row stride (Kc rounded up to 4)
+    int batch, tiles_w, tiles_h;   // small-channel kernel: pixel tiles of 16 x 32
     FastDiv dWo, dHo, dC, dKw;
 };
 
@@ -420,6 +421,140 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
     }
 }
 
+// ------------------------------------------------------------- small-channel weight gradient
+// 3x3/s1/p1 with C <= 16 input and N <= 16 output channels (configs C4/C5's 8/16-channel levels):
+// a GEMM with N, K this small wastes most of an MFMA tile, so each block sweeps 16 x 32 pixel
+// tiles (grid-stride), stages the input halo and the gradient tile in LDS, and accumulates
+// dW[n][tap][c] on the VALU: thread items = (tap, 4 output x 4 input channels) plus bias items
+// (4 output channels), replicated over pixel groups when the items do not fill the block.  The
+// block's partial goes to slab row [block][n][tap*C + c] (bias at column K) and the fixed-order
+// fp64 split reduction below finishes it - deterministic like the GEMM path.
+constexpr int SW_TH = 16, SW_TW = 32;
+
+template <int C, int N>
+__global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
+    constexpr int HH = SW_TH + 2, HWD = SW_TW + 2;
+    constexpr int CP = (C + 3) & ~3, C4 = CP / 4, N4 = N / 4;
+    constexpr int WITEMS = 9 * N4 * C4;
+    constexpr int ITEMS = WITEMS + N4;
+    constexpr int GROUPS = 256 / ITEMS;
+    static_assert(GROUPS >= 1, "items");
+    constexpr int HALO = HH * HWD * CP, GT = SW_TH * SW_TW * N;
+    constexpr int SMEM = (HALO + GT) > (GROUPS * ITEMS * 16) ? (HALO + GT) : (GROUPS * ITEMS * 16);
+    __shared__ __attribute__((aligned(16))) float smem[SMEM];
+    float* halo = smem;
+    float* gt = smem + HALO;
+
+    const int tid = threadIdx.x;
+    const int item = tid % ITEMS, grp = tid / ITEMS;
+    const bool active = grp < GROUPS;
+    const bool wi = item < WITEMS;
+    int tap = 0, co4 = 0, ci4 = 0;
+    if (wi) {
+        tap = item / (N4 * C4);
+        const int rem = item - tap * (N4 * C4);
+        co4 = rem / C4;
+        ci4 = rem - co4 * C4;
+    } else {
+        co4 = item - WITEMS;
+    }
+    const int tr = tap / 3, ts = tap - tr * 3;
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+
+    const int ntiles = p.batch * p.tiles_h * p.tiles_w;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int txi = t % p.tiles_w;
+        const int tyi = (t / p.tiles_w) % p.tiles_h;
+        const int b = t / (p.tiles_w * p.tiles_h);
+        const int y0 = tyi * SW_TH, x0 = txi * SW_TW;
+        const long long img = (long long)b * p.Hi * p.Wi;
+        __syncthreads();                       // previous tile's readers are done
+        for (int e = tid; e < HH * HWD * C4; e += 256) {
+            const int q = e % C4, pix = e / C4;
+            const int hx = pix % HWD, hy = pix / HWD;
+            const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
+                const long long px = img + (long long)gy * p.Wi + gx;
+                if (C % 4 == 0 && p.c0 % 4 == 0) {
+                    const int c = 4 * q;
+                    v = c < p.c0 ? *reinterpret_cast<const f32x4*>(p.src0 + px * p.c0 + c)
+                                 : *reinterpret_cast<const f32x4*>(p.src1 + px * p.c1 + (c - p.c0));
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int c = 4 * q + k;
+                        if (c < C) v[k] = c < p.c0 ? p.src0[px * p.c0 + c] : p.src1[px * p.c1 + (c - p.c0)];
+                    }
+                }
+            }
+            *reinterpret_cast<f32x4*>(halo + pix * CP + 4 * q) = v;
+        }
+        for (int e = tid; e < SW_TH * SW_TW * N4; e += 256) {
+            const int q = e % N4, pix = e / N4;
+            const int oy = y0 + pix / SW_TW, ox = x0 + pix % SW_TW;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (oy < p.Ho && ox < p.Wo)
+                v = *reinterpret_cast<const f32x4*>(p.P + ((long long)(b * p.Ho + oy) * p.Wo + ox) * N + 4 * q);
+            *reinterpret_cast<f32x4*>(gt + pix * N + 4 * q) = v;
+        }
+        __syncthreads();
+        if (active) {
+            if (wi) {
+                for (int pp = grp; pp < SW_TH * SW_TW; pp += GROUPS) {
+                    const int row = pp / SW_TW, col = pp - row * SW_TW;
+                    const f32x4 g4 = *reinterpret_cast<const f32x4*>(gt + pp * N + 4 * co4);
+                    const f32x4 x4 = *reinterpret_cast<const f32x4*>(halo + ((row + tr) * HWD + col + ts) * CP + 4 * ci4);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(g4[i], x4[j], acc[i][j]);
+                }
+            } else {
+                for (int pp = grp; pp < SW_TH * SW_TW; pp += GROUPS) {
+                    const f32x4 g4 = *reinterpret_cast<const f32x4*>(gt + pp * N + 4 * co4);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[0][i] += g4[i];
+                }
+            }
+        }
+    }
+    // fixed-order reduction over the pixel groups, then this block's slab rows
+    __syncthreads();
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) smem[(grp * ITEMS + item) * 16 + i * 4 + j] = acc[i][j];
+    }
+    __syncthreads();
+    if (tid < ITEMS) {
+        float v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = 0.f;
+        for (int g = 0; g < GROUPS; ++g)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] += smem[(g * ITEMS + tid) * 16 + e];
+        float* slab = p.slab + (long long)blockIdx.x * p.Nr * p.Kcp;
+        if (tid < WITEMS) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = 4 * ci4 + j;
+                    if (c < C) slab[(long long)(4 * co4 + i) * p.Kcp + tap * C + c] = v[i * 4 + j];
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) slab[(long long)(4 * co4 + i) * p.Kcp + p.K] = v[i];
+        }
+    }
+}
+
 // Split-K reduction, pass 1: part[g][idx] = sum over splits z = g, g+G, ... of slab[z][idx]
 // (fp64, 4 independent accumulators so each thread keeps several loads in flight).
 __global__ void wgrad_sum_splits_kernel(const float* __restrict__ slab, int splits, long long total, int G,
@@ -475,11 +610,23 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
 
 struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
-    bool qvec, dma;
+    bool qvec, dma, small;
+    int tiles_w, tiles_h;
     size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
     size_t part_bytes() const { return G > 1 ? (size_t)G * Nr * Kcp * sizeof(double) : 0; }
     size_t ws_bytes() const { return ((slab_bytes() + 255) / 256) * 256 + part_bytes(); }
 };
+
+#ifndef PU_NO_SMALLCONV
+#define PU_NO_SMALLCONV 0
+#endif
+static bool small_wgrad_ok(const pu_wgrad_args* a) {
+    const int C = a->c0 + a->c1;
+    return !PU_NO_SMALLCONV && (C == 1 || C == 4 || C == 8 || C == 12 || C == 16) &&
+           (a->n == 4 || a->n == 8 || a->n == 16) && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
+           a->in_h == a->out_h && a->in_w == a->out_w && a->bias_mode != 2 &&
+           (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
+}
 
 static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     PU_REQUIRE(a && a->batch > 0 && a->out_h > 0 && a->out_w > 0 && a->in_h > 0 && a->in_w > 0, "pu_wgrad: bad grid");
@@ -498,6 +645,7 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->Kc = pl->K + (a->bias_mode == 1 ? 1 : 0);
     pl->Kcp = (pl->Kc + 3) / 4 * 4;
     pl->qvec = (a->c0 % 4 == 0) && (a->c1 % 4 == 0);
+    pl->small = small_wgrad_ok(a);
     if (pl->qvec) {
         PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0, "pu_wgrad: sources must be 16-byte aligned");
     }
@@ -507,6 +655,20 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
 #else
     pl->dma = pl->qvec;
 #endif
+    if (pl->small) {                   // direct small-channel kernel: one slab row block per block
+        pl->tiles_w = ceil_div(a->out_w, SW_TW);
+        pl->tiles_h = ceil_div(a->out_h, SW_TH);
+        const long long ntiles = (long long)a->batch * pl->tiles_w * pl->tiles_h;
+        pl->splits = (int)(ntiles < 1024 ? ntiles : 1024);
+        pl->BN = a->n; pl->BK = pl->K; pl->gx = pl->gy = 1; pl->mps = 0; pl->dma = false;
+        const long long total = (long long)pl->Nr * pl->Kcp;
+        int G = (int)ceil_div(262144LL, total);
+        const int by_len = ceil_div(pl->splits, 8);
+        if (G > by_len) G = by_len;
+        if (G > 16) G = 16;
+        pl->G = G < 1 ? 1 : G;
+        return PU_OK;
+    }
     // the direct-to-LDS kernel tiles only the N x K GEMM (bias via LDS column sums); the
     // register-staged kernel carries the bias as an extra ones column / row
     const int ext_n = pl->dma ? a->n : pl->Nr;
@@ -562,7 +724,7 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
     if (st != PU_OK) return st;
     if (bn) *bn = pl.BN;
     if (bk) *bk = pl.BK;
-    if (qvec) *qvec = pl.qvec ? 1 : 0;
+    if (qvec) *qvec = pl.small ? 2 : (pl.qvec ? 1 : 0);   // 2: small-channel direct kernel
     if (splits) *splits = pl.splits;
     return PU_OK;
 }
@@ -592,6 +754,19 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
     hipStream_t s = as_stream(stream);
     p.gx = pl.gx;
     p.gy = pl.gy;
+    p.batch = a->batch; p.tiles_w = pl.tiles_w; p.tiles_h = pl.tiles_h;
+    if (pl.small && (phase & 1)) {
+        const int C = pl.C, N = a->n;
+        const dim3 sg(pl.splits);
+#define PU_SW(C_, N_) if (C == C_ && N == N_) hipLaunchKernelGGL((wgrad_small_kernel<C_, N_>), sg, dim3(256), 0, s, p)
+        PU_SW(1, 4); else PU_SW(1, 8); else PU_SW(1, 16); else PU_SW(4, 4); else PU_SW(4, 8); else PU_SW(4, 16);
+        else PU_SW(8, 4); else PU_SW(8, 8); else PU_SW(8, 16); else PU_SW(12, 4); else PU_SW(12, 8);
+        else PU_SW(12, 16); else PU_SW(16, 4); else PU_SW(16, 8); else PU_SW(16, 16);
+#undef PU_SW
+        st = check_launch("pu_wgrad (small-channel)");
+        if (st != PU_OK) return st;
+        phase &= ~1;
+    }
     dim3 grid(p.gx * p.gy * pl.splits);
     if (phase & 1) {
 #define PU_WG_DMA(BN_, BK_, WN_, WK_) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3>), grid, dim3(256), 0, s, p)

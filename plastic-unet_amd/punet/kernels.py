@@ -22,7 +22,7 @@ def lib():
 
 # ------------------------------------------------------------------------------ launch profiler
 _PROF = None
-_MODES = {0: "chunk16", 1: "vec4", 2: "scalar"}
+_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct"}
 
 
 class KernelProfiler:
@@ -141,8 +141,18 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
     L.pu_conv_igemm_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(mode), ctypes.byref(ks))
     M = batch * out_hw[0] * out_hw[1]
     tag = "igemm<%dx%d,%s%s>" % (bm.value, bn.value, _MODES[mode.value], ",k%d" % ks.value if ks.value > 1 else "")
-    with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
-        check(lib().pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
+    nb = 0.0
+    if mode.value == 3:    # direct small-channel kernel: HBM-bound, report its algorithmic bytes
+        per = (c0 + c1) + n * (1 + int(accum) + int(resid is not None)) + n0_mask(n, n0, mask0, mask1)
+        nb = 4.0 * M * per
+    with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1), nbytes=nb):
+        check(L.pu_conv_igemm(ctypes.byref(a), _stream()), "pu_conv_igemm")
+
+
+def n0_mask(n, n0, mask0, mask1):
+    """channels of the ReLU masks an igemm epilogue reads"""
+    n0 = n if n0 is None else n0
+    return (n0 if mask0 is not None else 0) + (n - n0 if mask1 is not None else 0)
 
 
 def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, src1=None, c1=0,
@@ -164,7 +174,7 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, "vec4" if qv.value else "scalar")
+    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct")[qv.value])
     # the GEMM and the split reduction timed apart (they are separate kernels in rocprof too)
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
         check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 1, _stream()), "pu_wgrad_phase")
