@@ -38,7 +38,7 @@ import torch.distributed as dist  # noqa: E402
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None, help="images per GPU (c2/c4: 32, c5: 16)")
@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--no-kernel-profile", action="store_true")
     ap.add_argument("--no-oja", action="store_true", help="skip the Oja-update HBM benchmark")
     a = ap.parse_args()
-    dflt = {"c2": (32, 128), "c4": (32, 256), "c5": (16, 512)}[a.config]
+    dflt = {"c2": (32, 128), "c3": (32, 128), "c4": (32, 256), "c5": (16, 512)}[a.config]
     a.batch = a.batch or dflt[0]
     a.img = a.img or dflt[1]
     return a
@@ -61,6 +61,8 @@ def parse():
 
 CONFIGS = {
     "c2": "C2: UNetp depth %(depth)d base_ch %(base)d, %(rule)s rule, 1x%(img)dx%(img)d, fwd+BCE+bwd+Adam",
+    "c3": "C3: UNetp depth %(depth)d base_ch %(base)d bf16 (fp32 accumulation / params / Adam / head), %(rule)s "
+          "rule, 1x%(img)dx%(img)d, fwd+BCE+bwd+Adam",
     "c4": "C4: CoordConv-UNet (coord_conv_script.py topology, with_r) base 8 depth 5 + plastic head, %(rule)s rule, "
           "1x%(img)dx%(img)d, fwd+BCE+bwd+Adam",
     "c5": "C5: UNetpRes neurons 8, Dropout2d 0.5 (train mode), %(rule)s rule, 1x%(img)dx%(img)d, fwd+BCE+bwd+Adam",
@@ -83,7 +85,8 @@ def build_model(args, device, ref=False):
         from unet import UNetpRes
         return UNetpRes(1, 1, device, neurons=8, rule=args.rule, nbf=args.img)
     from unet import UNetp
-    return UNetp(1, 1, device, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base)
+    return UNetp(1, 1, device, rule=args.rule, nbf=args.img, depth=args.depth, base_ch=args.base,
+                 precision="bf16" if args.config == "c3" else "fp32")
 
 
 def fp32_mfma_peak_tflops(kernels):
@@ -214,6 +217,10 @@ def main():
                 e["GB_s"] = round(d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1)
             kern[tag] = e
         peak, cu, clk = fp32_mfma_peak_tflops(K)
+        basis = "fp32 MFMA 256 FLOP/clk/CU x %d CU x %.2f GHz" % (cu, clk)
+        if args.config == "c3":     # v_mfma_f32_32x32x16_bf16: 4096 FLOP/clk/CU dense
+            peak *= 16.0
+            basis = "bf16 MFMA 4096 FLOP/clk/CU x %d CU x %.2f GHz (dense)" % (cu, clk)
         mfma = {t: d for t, d in summ.items() if d["flops"] and (t.startswith("igemm") or t.startswith("wgrad"))}
         dom = max(mfma.items(), key=lambda kv: kv[1]["ms"])
         dtag, dd = dom
@@ -228,7 +235,7 @@ def main():
                 "all_conv_mfma": {"achieved": round(tot_f / (tot_ms * 1e-3) / 1e12, 2),
                                   "frac": round(tot_f / (tot_ms * 1e-3) / 1e12 / peak, 4),
                                   "flop_per_step": tot_f / nprof, "ms_per_step": round(tot_ms / nprof, 3)},
-                "peak_basis": "fp32 MFMA 256 FLOP/clk/CU x %d CU x %.2f GHz" % (cu, clk)}
+                "peak_basis": basis}
         prof_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof_path):
             try:
@@ -259,7 +266,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16" if args.config == "c3" else "f32",
             "data": "synthetic: x~U[0,1) [B,1,%d,%d], targets (U>0.5); random init (seed 0)" % (S, S),
             "config": {"workload": CONFIGS[args.config] % vars(args),
                        "global_batch": world * B, "per_gpu_batch": B, "img": S,

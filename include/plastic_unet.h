@@ -203,6 +203,35 @@ int pu_outconv_bwd(const float* x, const float* w, const float* dy, float* dx, f
                    void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * bf16 mixed precision (config C3: "same model in bf16, fp32 accumulation").  Activations,
+ * gradients of activations, packed weights, masks and residuals are bf16 (void* below); bias,
+ * weight gradients, logits and the plastic head stay fp32.  Same argument structs and semantics
+ * as the fp32 entry points; v_mfma_f32_32x32x16_bf16 with fp32 accumulation, one rounding to
+ * bf16 in each epilogue.
+ *   pu_conv_igemm_bf16: channel counts multiple of 32, k_pad multiple of 32, cgroup 0 or 32,
+ *                       bias 16-byte aligned fp32.
+ *   pu_wgrad_bf16:      rows / src bf16 (channel counts and n multiples of 8), dweight / dbias fp32.
+ * ------------------------------------------------------------------------------------------- */
+int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream);
+size_t pu_conv_igemm_bf16_workspace_bytes(const pu_conv_args* a);
+int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit);
+size_t pu_wgrad_bf16_workspace_bytes(const pu_wgrad_args* a);
+int pu_wgrad_bf16(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);
+int pu_wgrad_bf16_phase(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, int phase, void* stream);
+int pu_pack_weight_bf16(const float* w, void* packed, int mode, int d0, int d1, int kh, int kw,
+                        int k_pad, int cgroup, void* stream);
+int pu_convert_f32_bf16(const float* x, void* y, long long n, void* stream);
+int pu_convert_bf16_f32(const void* x, float* y, long long n, void* stream);
+int pu_maxpool2_fwd_bf16(const void* x, void* y, int batch, int h, int w, int c, void* stream);
+int pu_maxpool2_bwd_bf16(const void* x, const void* dy, void* dx, int batch, int h, int w, int c,
+                         int relu_mask, int accumulate, void* stream);
+int pu_outconv_fwd_bf16(const void* x, const float* w, const float* b, float* y, long long rows, int c,
+                        void* stream);
+int pu_outconv_bwd_bf16(const void* x, const float* w, const float* dy, void* dx, float* dw, float* db,
+                        long long rows, int c, int relu_mask, void* workspace, size_t workspace_bytes,
+                        void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Plastic head (unet_p.py:69-88), batched over per-slot traces:
  *   Y_b = sigmoid(X_b (w + alpha (.) H_b))
  *   hebb rule (0): H'_b = (1-eta) H_b + eta x0 y0^T ;  oja rule (1): H'_b = H_b + eta (x0 - H_b y0) y0

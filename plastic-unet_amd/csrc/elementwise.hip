@@ -12,6 +12,20 @@
 namespace pu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// activation element access for the fp32 and bf16 (config C3) variants: compute is fp32
+template <typename T> __device__ __forceinline__ f32x4 ld4(const T* p);
+template <> __device__ __forceinline__ f32x4 ld4<float>(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+template <> __device__ __forceinline__ f32x4 ld4<__bf16>(const __bf16* p) {
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, f32x4 v);
+template <> __device__ __forceinline__ void st4<float>(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+template <> __device__ __forceinline__ void st4<__bf16>(__bf16* p, f32x4 v) {
+    *reinterpret_cast<bf16x4*>(p) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+}
 
 // K position -> tap-major index (tap*C + c) for a channel-group-major packed K axis
 __device__ __forceinline__ int ungroup_k(int k, int C, int taps, int G) {
@@ -21,7 +35,8 @@ __device__ __forceinline__ int ungroup_k(int k, int C, int taps, int G) {
     return tap * C + g * G + cg;
 }
 
-__global__ void pack_weight_kernel(const float* __restrict__ w, float* __restrict__ p, int mode, int d0, int d1,
+template <typename TO>
+__global__ void pack_weight_kernel(const float* __restrict__ w, TO* __restrict__ p, int mode, int d0, int d1,
                                    int kh, int kw, int k_pad, int rows, int G) {
     const long long total = (long long)rows * k_pad;
     const int taps = kh * kw;
@@ -65,7 +80,7 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, float* __restric
                 if (r >= 0 && q >= 0) v = w[(((long long)i * d1 + o) * 3 + r) * 3 + q];
             }
         }
-        p[idx] = v;
+        p[idx] = (TO)v;
     }
 }
 
@@ -88,8 +103,8 @@ __device__ __forceinline__ void pool_take(float v, int idx, float& best, int& ar
     }
 }
 
-template <bool VEC>
-__global__ void maxpool_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int H, int W, int C, int Ho,
+template <bool VEC, typename T = float>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int H, int W, int C, int Ho,
                                    int Wo, long long total) {
     const int CV = VEC ? C / 4 : C;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -106,28 +121,28 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ x, float* __restric
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const long long pix = base + (q >> 1) * W + (q & 1);
-                f32x4 v = *reinterpret_cast<const f32x4*>(x + pix * C + cv * 4);
+                f32x4 v = ld4(x + pix * C + cv * 4);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) { float bb = best[e]; pool_take(v[e], q, bb, arg[e]); best[e] = bb; }
             }
-            *reinterpret_cast<f32x4*>(y + idx * 4) = best;
+            st4(y + idx * 4, best);
         } else {
             float best = -INFINITY;
             int arg = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const long long pix = base + (q >> 1) * W + (q & 1);
-                pool_take(x[pix * C + cv], q, best, arg);
+                pool_take((float)x[pix * C + cv], q, best, arg);
             }
-            y[idx] = best;
+            y[idx] = (T)best;
         }
     }
 }
 
 // One thread per INPUT element group (pixel, 4 channels): recompute the window's argmax and
 // route the pooled gradient to it; every other input element gets 0 (or keeps its value).
-template <bool VEC>
-__global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, float* __restrict__ dx,
+template <bool VEC, typename T = float>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
                                    int H, int W, int C, int Ho, int Wo, int relu_mask, int accumulate,
                                    long long total) {
     constexpr int V = VEC ? 4 : 1;
@@ -144,7 +159,7 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __r
         float old[V];
         if (accumulate) {
 #pragma unroll
-            for (int e = 0; e < V; ++e) old[e] = dx[idx * V + e];
+            for (int e = 0; e < V; ++e) old[e] = (float)dx[idx * V + e];
         }
 #pragma unroll
         for (int e = 0; e < V; ++e) out[e] = 0.f;
@@ -161,7 +176,7 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __r
                 const long long pix = base + (q >> 1) * W + (q & 1);
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
-                    float v = x[pix * C + cv * V + e];
+                    float v = (float)x[pix * C + cv * V + e];
                     if (q == me) xme[e] = v;
                     pool_take(v, q, best[e], arg[e]);
                 }
@@ -169,16 +184,17 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __r
             const long long oidx = ((b * Ho + ho) * Wo + wo) * C + cv * V;
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                if (arg[e] == me && (!relu_mask || xme[e] > 0.f)) out[e] = dy[oidx + e];
+                if (arg[e] == me && (!relu_mask || xme[e] > 0.f)) out[e] = (float)dy[oidx + e];
             }
         }
 #pragma unroll
-        for (int e = 0; e < V; ++e) dx[idx * V + e] = accumulate ? old[e] + out[e] : out[e];
+        for (int e = 0; e < V; ++e) dx[idx * V + e] = (T)(accumulate ? old[e] + out[e] : out[e]);
     }
 }
 
 // outconv forward: 16 lanes per pixel, each a float4 of channels; shuffle-reduce over the 16.
-__global__ void outconv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+template <typename T = float>
+__global__ void outconv_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
                                    float* __restrict__ y, long long rows, int C) {
     const int lane16 = threadIdx.x & 15;
     const long long groups = (long long)gridDim.x * (blockDim.x >> 4);
@@ -186,7 +202,7 @@ __global__ void outconv_fwd_kernel(const float* __restrict__ x, const float* __r
     for (long long m = blockIdx.x * (long long)(blockDim.x >> 4) + (threadIdx.x >> 4); m < rows + 0; m += groups) {
         float s = 0.f;
         for (int c = lane16 * 4; c < C; c += 64) {
-            f32x4 v = *reinterpret_cast<const f32x4*>(x + m * C + c);
+            f32x4 v = ld4(x + m * C + c);
             f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
             s += v[0] * ww[0] + v[1] * ww[1] + v[2] * ww[2] + v[3] * ww[3];
         }
@@ -211,8 +227,9 @@ __global__ void outconv_fwd_scalar_kernel(const float* __restrict__ x, const flo
 // Thread layout: 16 pixel groups x 16 lanes; lane owns channels lane*4 + 64*j.
 constexpr int OC_BLOCKS = 1024;
 
-__global__ void outconv_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ dy,
-                                   float* __restrict__ dx, float* __restrict__ partial, long long rows, int C,
+template <typename T = float>
+__global__ void outconv_bwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ dy,
+                                   T* __restrict__ dx, float* __restrict__ partial, long long rows, int C,
                                    int relu_mask) {
     __shared__ float red[16][65];
     __shared__ float redb[16];
@@ -226,12 +243,12 @@ __global__ void outconv_bwd_kernel(const float* __restrict__ x, const float* __r
             const float g = dy[m];
             ab += g;
             if (c < C) {
-                f32x4 v = *reinterpret_cast<const f32x4*>(x + m * C + c);
+                f32x4 v = ld4(x + m * C + c);
                 f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
                 f32x4 o;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] = (!relu_mask || v[e] > 0.f) ? g * ww[e] : 0.f;
-                *reinterpret_cast<f32x4*>(dx + m * C + c) = o;
+                st4(dx + m * C + c, o);
                 a0 += g * v[0]; a1 += g * v[1]; a2 += g * v[2]; a3 += g * v[3];
             }
         }
@@ -418,20 +435,31 @@ static int grid_for(long long total, int block = 256, int cap = 8192) {
     return (int)g;
 }
 
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, __bf16* __restrict__ y, long long n4) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
+        st4(y + 4 * i, ld4(x + 4 * i));
+}
+
+__global__ void bf16_to_f32_kernel(const __bf16* __restrict__ x, float* __restrict__ y, long long n4) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
+        st4(y + 4 * i, ld4(x + 4 * i));
+}
+
 }  // namespace pu
 
 using namespace pu;
 
-extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw, int k_pad,
-                              int cgroup, void* stream) {
-    PU_REQUIRE(w && packed && d0 > 0 && d1 > 0 && kh > 0 && kw > 0 && k_pad > 0, "pu_pack_weight: bad args");
-    PU_REQUIRE(cgroup == 0 || cgroup == 16 || cgroup == 32, "pu_pack_weight: cgroup %d", cgroup);
+template <typename TO>
+static int pack_weight_impl(const float* w, TO* packed, int mode, int d0, int d1, int kh, int kw, int k_pad, int cgroup,
+                            void* stream, const char* name) {
+    PU_REQUIRE(w && packed && d0 > 0 && d1 > 0 && kh > 0 && kw > 0 && k_pad > 0, "%s: bad args", name);
+    PU_REQUIRE(cgroup == 0 || cgroup == 16 || cgroup == 32, "%s: cgroup %d", name, cgroup);
     if (cgroup) {
         const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;
-        PU_REQUIRE(mode == PU_PACK_CONVT_FWD || Ck % cgroup == 0, "pu_pack_weight: %d channels not a multiple of cgroup %d", Ck, cgroup);
+        PU_REQUIRE(mode == PU_PACK_CONVT_FWD || Ck % cgroup == 0, "%s: %d channels not a multiple of cgroup %d", name, Ck, cgroup);
     }
-    PU_REQUIRE(mode >= 0 && mode <= 4, "pu_pack_weight: mode %d", mode);
-    PU_REQUIRE(mode != PU_PACK_CONVT3_FWD || (kh == 3 && kw == 3 && cgroup == 0), "pu_pack_weight: CONVT3_FWD is 3x3, tap-major");
+    PU_REQUIRE(mode >= 0 && mode <= 4, "%s: mode %d", name, mode);
+    PU_REQUIRE(mode != PU_PACK_CONVT3_FWD || (kh == 3 && kw == 3 && cgroup == 0), "%s: CONVT3_FWD is 3x3, tap-major", name);
     const int taps = kh * kw;
     int rows, kmin;
     switch (mode) {
@@ -441,11 +469,21 @@ extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, i
         case PU_PACK_CONVT3_FWD: rows = 4 * d1; kmin = 4 * d0; break;
         default: rows = d0; kmin = taps * d1; break;
     }
-    PU_REQUIRE(k_pad >= kmin, "pu_pack_weight: k_pad %d < %d", k_pad, kmin);
+    PU_REQUIRE(k_pad >= kmin, "%s: k_pad %d < %d", name, k_pad, kmin);
     const long long total = (long long)rows * k_pad;
-    hipLaunchKernelGGL(pack_weight_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), w, packed, mode, d0,
-                       d1, kh, kw, k_pad, rows, cgroup);
-    return check_launch("pu_pack_weight");
+    hipLaunchKernelGGL(pack_weight_kernel<TO>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), w, packed, mode,
+                       d0, d1, kh, kw, k_pad, rows, cgroup);
+    return check_launch(name);
+}
+
+extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw, int k_pad,
+                              int cgroup, void* stream) {
+    return pack_weight_impl(w, packed, mode, d0, d1, kh, kw, k_pad, cgroup, stream, "pu_pack_weight");
+}
+
+extern "C" int pu_pack_weight_bf16(const float* w, void* packed, int mode, int d0, int d1, int kh, int kw, int k_pad,
+                                   int cgroup, void* stream) {
+    return pack_weight_impl(w, (__bf16*)packed, mode, d0, d1, kh, kw, k_pad, cgroup, stream, "pu_pack_weight_bf16");
 }
 
 extern "C" int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, void* stream) {
@@ -490,7 +528,7 @@ extern "C" int pu_outconv_fwd(const float* x, const float* w, const float* b, fl
     PU_REQUIRE(x && w && y && rows > 0 && c > 0, "pu_outconv_fwd: bad args");
     if (c % 4 == 0 && (((uintptr_t)x | (uintptr_t)w) & 15) == 0) {
         const long long groups = (rows + 15) / 16;
-        hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for(groups, 1, 8192)), dim3(256), 0, as_stream(stream), x, w,
+        hipLaunchKernelGGL(outconv_fwd_kernel<float>, dim3(grid_for(groups, 1, 8192)), dim3(256), 0, as_stream(stream), x, w,
                            b, y, rows, c);
     } else {
         hipLaunchKernelGGL(outconv_fwd_scalar_kernel, dim3(grid_for(rows)), dim3(256), 0, as_stream(stream), x, w, b, y,
@@ -514,7 +552,7 @@ extern "C" int pu_outconv_bwd(const float* x, const float* w, const float* dy, f
     int blocks = (int)((rows + 15) / 16);
     if (blocks > OC_BLOCKS) blocks = OC_BLOCKS;
     float* part = (float*)workspace;
-    hipLaunchKernelGGL(outconv_bwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, w, dy, dx, part, rows, c,
+    hipLaunchKernelGGL(outconv_bwd_kernel<float>, dim3(blocks), dim3(256), 0, as_stream(stream), x, w, dy, dx, part, rows, c,
                        relu_mask);
     hipLaunchKernelGGL(column_sum_kernel, dim3(c + 1), dim3(256), 0, as_stream(stream), part, blocks, c, dw, db);
     return check_launch("pu_outconv_bwd");
@@ -565,4 +603,59 @@ extern "C" int pu_add_coords(const float* x, float* out, int batch, int c, int h
     hipLaunchKernelGGL(add_coords_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, out, c, h, w,
                        with_r, total);
     return check_launch("pu_add_coords");
+}
+
+// ------------------------------------------------------------------ bf16 variants (config C3)
+extern "C" int pu_convert_f32_bf16(const float* x, void* y, long long n, void* stream) {
+    PU_REQUIRE(x && y && n > 0 && n % 4 == 0, "pu_convert_f32_bf16: n %lld must be a positive multiple of 4", n);
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream), x, (__bf16*)y, n / 4);
+    return check_launch("pu_convert_f32_bf16");
+}
+
+extern "C" int pu_convert_bf16_f32(const void* x, float* y, long long n, void* stream) {
+    PU_REQUIRE(x && y && n > 0 && n % 4 == 0, "pu_convert_bf16_f32: n %lld must be a positive multiple of 4", n);
+    hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream), (const __bf16*)x, y, n / 4);
+    return check_launch("pu_convert_bf16_f32");
+}
+
+extern "C" int pu_maxpool2_fwd_bf16(const void* x, void* y, int batch, int h, int w, int c, void* stream) {
+    PU_REQUIRE(x && y && batch > 0 && h >= 2 && w >= 2 && c > 0 && c % 4 == 0, "pu_maxpool2_fwd_bf16: bad args");
+    const int ho = h / 2, wo = w / 2;
+    const long long total = (long long)batch * ho * wo * (c / 4);
+    hipLaunchKernelGGL((maxpool_fwd_kernel<true, __bf16>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                       (const __bf16*)x, (__bf16*)y, h, w, c, ho, wo, total);
+    return check_launch("pu_maxpool2_fwd_bf16");
+}
+
+extern "C" int pu_maxpool2_bwd_bf16(const void* x, const void* dy, void* dx, int batch, int h, int w, int c,
+                                    int relu_mask, int accumulate, void* stream) {
+    PU_REQUIRE(x && dy && dx && batch > 0 && h >= 2 && w >= 2 && c > 0 && c % 4 == 0, "pu_maxpool2_bwd_bf16: bad args");
+    const int ho = h / 2, wo = w / 2;
+    const long long total = (long long)batch * h * w * (c / 4);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<true, __bf16>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
+                       (const __bf16*)x, (const __bf16*)dy, (__bf16*)dx, h, w, c, ho, wo, relu_mask, accumulate, total);
+    return check_launch("pu_maxpool2_bwd_bf16");
+}
+
+extern "C" int pu_outconv_fwd_bf16(const void* x, const float* w, const float* b, float* y, long long rows, int c,
+                                   void* stream) {
+    PU_REQUIRE(x && w && y && rows > 0 && c > 0 && c % 4 == 0, "pu_outconv_fwd_bf16: bad args");
+    const long long groups = (rows + 15) / 16;
+    hipLaunchKernelGGL(outconv_fwd_kernel<__bf16>, dim3(grid_for(groups, 1, 8192)), dim3(256), 0, as_stream(stream),
+                       (const __bf16*)x, w, b, y, rows, c);
+    return check_launch("pu_outconv_fwd_bf16");
+}
+
+extern "C" int pu_outconv_bwd_bf16(const void* x, const float* w, const float* dy, void* dx, float* dw, float* db,
+                                   long long rows, int c, int relu_mask, void* workspace, size_t ws_bytes, void* stream) {
+    PU_REQUIRE(x && w && dy && dx && dw && db && rows > 0 && c % 4 == 0, "pu_outconv_bwd_bf16: bad args");
+    const size_t need = pu_outconv_workspace_bytes(rows, c);
+    if (!workspace || ws_bytes < need) return fail(PU_ERR_WORKSPACE, "pu_outconv_bwd_bf16: workspace %zu < %zu", ws_bytes, need);
+    int blocks = (int)((rows + 15) / 16);
+    if (blocks > OC_BLOCKS) blocks = OC_BLOCKS;
+    float* part = (float*)workspace;
+    hipLaunchKernelGGL(outconv_bwd_kernel<__bf16>, dim3(blocks), dim3(256), 0, as_stream(stream), (const __bf16*)x, w,
+                       dy, (__bf16*)dx, part, rows, c, relu_mask);
+    hipLaunchKernelGGL(column_sum_kernel, dim3(c + 1), dim3(256), 0, as_stream(stream), part, blocks, c, dw, db);
+    return check_launch("pu_outconv_bwd_bf16");
 }

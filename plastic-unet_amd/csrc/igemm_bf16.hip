@@ -1,0 +1,419 @@
+// bf16 mixed-precision implicit-GEMM convolution (config C3: "same model in bf16, fp32
+// accumulation").  Activations, weights, masks and residuals are bf16 in HBM;
+// v_mfma_f32_32x32x16_bf16 accumulates in fp32; bias is fp32; outputs are rounded to bf16 once, in
+// the epilogue.
+//
+// Same machinery as igemm.hip's direct-to-LDS kernel, byte for byte: a stage is 64-byte LDS rows
+// filled by global_load_lds_dwordx4 with the XOR swizzle kc ^ ((r>>2)&3), a 3-deep ring, counted
+// vmcnt + raw barrier, branch-free loader.  A 64-byte row now holds 32 bf16 k-values (BK = 32) and
+// a lane's 16-byte chunk is exactly one 32x32x16 operand fragment (8 consecutive k of its row:
+// A[row l&31][k = 8h + j], B[k = 8h + j][col l&31]), so each (i, j) sub-tile takes 2 MFMAs per
+// stage.  Weights are the A operand, pixels the B operand: each lane owns 4 consecutive output
+// channels of one pixel, stored as 8 bytes.
+#include "common.h"
+
+namespace pu {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK16 = 32;   // k per stage (64 B of bf16)
+
+struct IgemmBf16Params {
+    int M, N, K, k_pad;
+    int Hi, Wi, Ho, Wo, kh, kw, stride, pad;
+    int C, c0, c1;
+    const __bf16* src0;
+    const __bf16* src1;
+    const __bf16* wt;
+    const float* bias;
+    __bf16* dst0;
+    __bf16* dst1;
+    const __bf16* mask0;
+    const __bf16* mask1;
+    const __bf16* resid;
+    int n0, flags;
+    int cgroup, taps, gn;
+    int ksplit, t_per;
+    float* part;
+    int shuf_h, shuf_w, shuf_off;
+    FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
+};
+
+struct EpiRowB {
+    long long pix;
+    int oh0, ow0;
+};
+
+__device__ __forceinline__ EpiRowB epi_row_b(const IgemmBf16Params& p, int m) {
+    if (!(p.flags & PU_EPI_SHUFFLE2)) return {m, 0, 0};
+    const int t2 = fdiv(m, p.dWo);
+    const int wo = m - t2 * p.Wo;
+    const int bb = fdiv(t2, p.dHo);
+    const int ho = t2 - bb * p.Ho;
+    return {(long long)bb * p.shuf_h, 2 * ho - p.shuf_off, 2 * wo - p.shuf_off};
+}
+
+__device__ __forceinline__ f32x4 ld4(const __bf16* p) {
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+// epilogue of output channels n..n+3 (n % 4 == 0, N % 4 == 0, n0 % 4 == 0) of row r
+__device__ __forceinline__ void epi_store4_b(const IgemmBf16Params& p, const EpiRowB& r, int n, f32x4 v) {
+    __bf16* dst;
+    const __bf16* msk;
+    long long off;
+    int nb;
+    if (p.flags & PU_EPI_SHUFFLE2) {
+        const int co = p.N >> 2;
+        const int ij = fdiv(n, p.dCo);
+        nb = n - ij * co;
+        const int oh = r.oh0 + (ij >> 1), ow = r.ow0 + (ij & 1);
+        if ((unsigned)oh >= (unsigned)p.shuf_h || (unsigned)ow >= (unsigned)p.shuf_w) return;
+        off = ((r.pix + oh) * p.shuf_w + ow) * co + nb;
+        dst = p.dst0; msk = p.mask0;
+    } else if (n < p.n0) {
+        off = r.pix * p.n0 + n;
+        dst = p.dst0; msk = p.mask0; nb = n;
+    } else {
+        off = r.pix * (p.N - p.n0) + (n - p.n0);
+        dst = p.dst1; msk = p.mask1; nb = n;
+    }
+    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + nb);
+    if (p.resid) v += ld4(p.resid + off);
+    if (p.flags & PU_EPI_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (msk) {
+        const f32x4 mv = ld4(msk + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
+    }
+    if (p.flags & PU_EPI_ACCUM) v += ld4(dst + off);
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+    *reinterpret_cast<bf16x4*>(dst + off) = o;
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+__device__ __attribute__((aligned(16))) __bf16 g_zero_b16[8];
+
+template <int BM, int BN, int WM, int WN, int NBUF>
+__global__ __launch_bounds__(256) void igemm_bf16_kernel(const IgemmBf16Params p) {
+    constexpr int FM = BM / WM / 32;
+    constexpr int FN = BN / WN / 32;
+    constexpr int A_LD = BM / 64;
+    constexpr int B_LD = BN / 64;
+    constexpr int G = A_LD + B_LD;
+    constexpr int STAGE = (BM + BN) * BK16;   // bf16 elements per ring slot (64 B per row)
+    static_assert(WM * WN == 4, "4 waves");
+
+    __shared__ __attribute__((aligned(16))) __bf16 lds[NBUF * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int lr = lane & 31, lh = lane >> 5;
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kz = tile / (gridDim.x / p.ksplit);
+    tile -= kz * (gridDim.x / p.ksplit);
+    const int mb = tile / p.gn;
+    const int m_blk = mb * BM;
+    const int n_blk = (tile - mb * p.gn) * BN;
+
+    const int lq = lane >> 2;
+    const int kc = (lane & 3) ^ ((lane >> 4) & 3);   // logical 16-B chunk this lane fetches
+    long long rb0[A_LD], rb1[A_LD];
+    unsigned tmask[A_LD];
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) {
+        const int m = m_blk + wave * (BM / 4) + 16 * j + lq;
+        rb0[j] = 0; rb1[j] = 0; tmask[j] = 0;
+        if (m < p.M) {
+            const int t = fdiv(m, p.dWo);
+            const int wo = m - t * p.Wo;
+            const int b = fdiv(t, p.dHo);
+            const int ho = t - b * p.Ho;
+            const int hb = ho * p.stride - p.pad, wb = wo * p.stride - p.pad;
+            const long long pix0 = (long long)b * p.Hi * p.Wi + (long long)hb * p.Wi + wb;
+            rb0[j] = pix0 * p.c0 + kc * 8;
+            rb1[j] = pix0 * p.c1 + kc * 8;
+            unsigned msk = 0;
+            for (int r = 0; r < p.kh; ++r)
+                for (int q = 0; q < p.kw; ++q)
+                    if ((unsigned)(hb + r) < (unsigned)p.Hi && (unsigned)(wb + q) < (unsigned)p.Wi)
+                        msk |= 1u << (r * p.kw + q);
+            tmask[j] = msk;
+        }
+    }
+    const __bf16* wrow[B_LD];
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+        const int n = n_blk + wave * (BN / 4) + 16 * j + lq;
+        wrow[j] = n < p.N ? p.wt + (long long)n * p.k_pad + kc * 8 : nullptr;
+    }
+
+    const int t0 = kz * p.t_per;
+    const int T = min(p.k_pad / BK16 - t0, p.t_per);
+    auto issue = [&](int tl, int slot) {
+        const bool live = tl < T;
+        const int t = t0 + (live ? tl : 0);
+        const int k0 = t * BK16;
+        // one stage = 32 consecutive channels of one tap (C % 32 == 0): tap-major, or 32-channel
+        // groups (cgroup 32: k = (g*taps + tap)*32 + c%32)
+        const int g = fdiv(t, p.dTaps);
+        const int tap_n = fdiv(k0, p.dC);
+        const int tap = p.cgroup ? t - g * p.taps : tap_n;
+        const int c = p.cgroup ? g * 32 : k0 - tap_n * p.C;
+        const int r = fdiv(tap, p.dKw);
+        const int s = tap - r * p.kw;
+        const bool first = c < p.c0;
+        const __bf16* src = first ? p.src0 : p.src1;
+        const int cs = first ? p.c0 : p.c1;
+        const long long off = (long long)(r * p.Wi + s) * cs + (first ? c : c - p.c0);
+        const unsigned bit = (live && k0 < p.K) ? (1u << tap) : 0u;
+        __bf16* a_slot = lds + slot * STAGE;
+        __bf16* b_slot = a_slot + BM * BK16;
+#pragma unroll
+        for (int j = 0; j < A_LD; ++j) {
+            const __bf16* gp = (tmask[j] & bit) ? src + (first ? rb0[j] : rb1[j]) + off : g_zero_b16;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)gp, (lds_void_t*)(a_slot + (wave * (BM / 4) + 16 * j) * BK16),
+                                             16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < B_LD; ++j) {
+            const __bf16* gp = (live && wrow[j]) ? wrow[j] + k0 : g_zero_b16;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)gp, (lds_void_t*)(b_slot + (wave * (BN / 4) + 16 * j) * BK16),
+                                             16, 0, 0);
+        }
+    };
+
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int a_row0 = wm * (BM / WM) + lr;
+    const int b_row0 = wn * (BN / WN) + lr;
+    const int swz = (lr >> 2) & 3;
+
+#pragma unroll
+    for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(s0, s0);
+
+    for (int t = 0; t < T; ++t) {
+        if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+        __builtin_amdgcn_s_barrier();
+        const __bf16* a = lds + (t % NBUF) * STAGE;
+        const __bf16* b = a + BM * BK16;
+        bf16x8 fa[2][FM], fb[2][FN];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int pos = ((kk * 2 + lh) ^ swz) * 8;
+#pragma unroll
+            for (int i = 0; i < FM; ++i) fa[kk][i] = *reinterpret_cast<const bf16x8*>(a + (a_row0 + i * 32) * BK16 + pos);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) fb[kk][j] = *reinterpret_cast<const bf16x8*>(b + (b_row0 + j * 32) * BK16 + pos);
+        }
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[kk][j], fa[kk][i], acc[i][j], 0, 0, 0);
+            if (kk == 0) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * (FM + FN), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * FM * FN, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if (p.ksplit > 1) {
+        float* part = p.part + (long long)kz * p.M * p.N;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+            if (m >= p.M) continue;
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                    if (n >= p.N) continue;
+                    f32x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                    *reinterpret_cast<f32x4*>(part + (long long)m * p.N + n) = v;
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+        if (m >= p.M) continue;
+        const EpiRowB er = epi_row_b(p, m);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                if (n >= p.N) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                epi_store4_b(p, er, n, v);
+            }
+    }
+}
+
+__global__ __launch_bounds__(256) void igemm_bf16_splitk_epilogue_kernel(const IgemmBf16Params p) {
+    const int nq = p.N >> 2;
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (long long)p.M * nq) return;
+    const int m = (int)(idx / nq);
+    const int n = (int)(idx - (long long)m * nq) * 4;
+    const long long mn = (long long)p.M * p.N;
+    const float* src = p.part + (long long)m * p.N + n;
+    f32x4 v = *reinterpret_cast<const f32x4*>(src);
+    for (int z = 1; z < p.ksplit; ++z) v += *reinterpret_cast<const f32x4*>(src + z * mn);
+    epi_store4_b(p, epi_row_b(p, m), n, v);
+}
+
+static int blocks_for_b(long long M, int N, int bm, int bn) { return ceil_div(M, bm) * ceil_div(N, bn); }
+
+static void choose_tile_b(long long M, int N, int* bm, int* bn) {
+    const int target = 480;
+    if (N <= 64) {
+        if (blocks_for_b(M, N, 256, 64) >= target) { *bm = 256; *bn = 64; }
+        else if (blocks_for_b(M, N, 128, 64) >= target) { *bm = 128; *bn = 64; }
+        else { *bm = 64; *bn = 64; }
+    } else {
+        if (blocks_for_b(M, N, 128, 128) >= target) { *bm = 128; *bn = 128; }
+        else if (blocks_for_b(M, N, 128, 64) >= target) { *bm = 128; *bn = 64; }
+        else { *bm = 64; *bn = 64; }
+    }
+}
+
+static void plan_split_b(const pu_conv_args* a, long long M, int bm, int bn, int* ksplit, int* t_per) {
+    const int T = a->k_pad / BK16;
+    *ksplit = 1;
+    *t_per = T;
+    const int occ = (bm == 256) ? 2 : (bm == 128 && bn == 128) ? 3 : 4;
+    const int blocks = blocks_for_b(M, a->n, bm, bn);
+    int ks = (256 * occ) / blocks;
+    if (ks > T / 4) ks = T / 4;
+    if (ks < 2) return;
+    *t_per = ceil_div(T, ks);
+    *ksplit = ceil_div(T, *t_per);
+}
+
+static int setup_bf16(const pu_conv_args* a, IgemmBf16Params* pp, long long* Mout) {
+    PU_REQUIRE(a != nullptr, "pu_conv_igemm_bf16: null args");
+    PU_REQUIRE(a->batch > 0 && a->in_h > 0 && a->in_w > 0 && a->out_h > 0 && a->out_w > 0, "pu_conv_igemm_bf16: bad grid");
+    PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0 && a->kh * a->kw <= 32, "pu_conv_igemm_bf16: bad taps");
+    PU_REQUIRE(a->src0 && a->weight && a->dst0 && a->n > 0, "pu_conv_igemm_bf16: operands");
+    PU_REQUIRE(a->c0 % 32 == 0 && a->c1 % 32 == 0 && a->c0 > 0 && (a->c1 == 0 || a->src1),
+               "pu_conv_igemm_bf16: channel counts (%d, %d) must be multiples of 32", a->c0, a->c1);
+    PU_REQUIRE(a->cgroup == 0 || a->cgroup == 32, "pu_conv_igemm_bf16: cgroup must be 0 or 32");
+    const int C = a->c0 + a->c1;
+    const int K = a->kh * a->kw * C;
+    PU_REQUIRE(a->k_pad >= K && a->k_pad % BK16 == 0, "pu_conv_igemm_bf16: k_pad %d (K %d) must be a multiple of 32", a->k_pad, K);
+    const bool shuffle = a->flags & PU_EPI_SHUFFLE2;
+    const int n0 = shuffle ? a->n : a->n0;
+    PU_REQUIRE(a->n % 4 == 0 && n0 % 4 == 0 && (!shuffle || (a->n / 4) % 4 == 0), "pu_conv_igemm_bf16: channel alignment");
+    PU_REQUIRE(shuffle || (n0 > 0 && n0 <= a->n && (n0 == a->n || a->dst1)), "pu_conv_igemm_bf16: n0 / dst1");
+    PU_REQUIRE(!(a->flags & PU_EPI_RESID) || (a->resid && !shuffle && n0 == a->n), "pu_conv_igemm_bf16: RESID");
+    const uintptr_t al = (uintptr_t)a->src0 | (uintptr_t)a->src1 | (uintptr_t)a->weight;
+    PU_REQUIRE((al & 15) == 0, "pu_conv_igemm_bf16: sources / weight must be 16-byte aligned");
+    const uintptr_t ae = (uintptr_t)a->dst0 | (uintptr_t)a->dst1 | (uintptr_t)a->mask0 | (uintptr_t)a->mask1 |
+                         (uintptr_t)a->resid;
+    PU_REQUIRE((ae & 7) == 0 && ((uintptr_t)a->bias & 15) == 0, "pu_conv_igemm_bf16: epilogue alignment");
+    const long long M = (long long)a->batch * a->out_h * a->out_w;
+    PU_REQUIRE(M < (1LL << 31), "pu_conv_igemm_bf16: too many pixels");
+    IgemmBf16Params& p = *pp;
+    p.M = (int)M; p.N = a->n; p.K = K; p.k_pad = a->k_pad;
+    p.Hi = a->in_h; p.Wi = a->in_w; p.Ho = a->out_h; p.Wo = a->out_w;
+    p.kh = a->kh; p.kw = a->kw; p.stride = a->stride; p.pad = a->pad;
+    p.C = C; p.c0 = a->c0; p.c1 = a->c1;
+    p.src0 = (const __bf16*)a->src0; p.src1 = (const __bf16*)a->src1; p.wt = (const __bf16*)a->weight;
+    p.bias = a->bias;
+    p.dst0 = (__bf16*)a->dst0; p.dst1 = (__bf16*)a->dst1;
+    p.mask0 = (const __bf16*)a->mask0; p.mask1 = (const __bf16*)a->mask1;
+    p.resid = (a->flags & PU_EPI_RESID) ? (const __bf16*)a->resid : nullptr;
+    p.n0 = n0; p.flags = a->flags;
+    p.cgroup = a->cgroup; p.taps = a->kh * a->kw;
+    p.shuf_h = a->shuf_h ? a->shuf_h : 2 * a->out_h;
+    p.shuf_w = a->shuf_w ? a->shuf_w : 2 * a->out_w;
+    p.shuf_off = a->shuf_off;
+    p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
+    p.dC = make_fastdiv(C); p.dKw = make_fastdiv(a->kw); p.dCo = make_fastdiv(shuffle ? a->n / 4 : 1);
+    p.dTaps = make_fastdiv(p.taps);
+    *Mout = M;
+    return PU_OK;
+}
+
+}  // namespace pu
+
+using namespace pu;
+
+extern "C" size_t pu_conv_igemm_bf16_workspace_bytes(const pu_conv_args* a) {
+    IgemmBf16Params p;
+    long long M;
+    if (setup_bf16(a, &p, &M) != PU_OK) return 0;
+    int bm, bn, ks, tp;
+    choose_tile_b(M, a->n, &bm, &bn);
+    plan_split_b(a, M, bm, bn, &ks, &tp);
+    return ks > 1 ? (size_t)ks * (size_t)M * (size_t)a->n * sizeof(float) : 0;
+}
+
+extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
+    IgemmBf16Params p;
+    long long M;
+    int st = setup_bf16(a, &p, &M);
+    if (st != PU_OK) return st;
+    const int N = a->n;
+    int bm, bn;
+    choose_tile_b(M, N, &bm, &bn);
+    p.gn = ceil_div(N, bn);
+    plan_split_b(a, M, bm, bn, &p.ksplit, &p.t_per);
+    if (p.ksplit > 1 && (!a->workspace || a->ws_bytes < (size_t)p.ksplit * M * N * sizeof(float))) {
+        p.ksplit = 1;
+        p.t_per = a->k_pad / BK16;
+    }
+    p.part = (float*)a->workspace;
+    hipStream_t s = as_stream(stream);
+    const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
+    if (bm == 256) hipLaunchKernelGGL((igemm_bf16_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
+    else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_bf16_kernel<128, 128, 2, 2, 3>), grid, dim3(256), 0, s, p);
+    else if (bm == 128) hipLaunchKernelGGL((igemm_bf16_kernel<128, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((igemm_bf16_kernel<64, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
+    if (p.ksplit > 1) {
+        const long long threads = M * (N / 4);
+        hipLaunchKernelGGL(igemm_bf16_splitk_epilogue_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, p);
+    }
+    return check_launch("pu_conv_igemm_bf16");
+}
+
+extern "C" int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit) {
+    IgemmBf16Params p;
+    long long M;
+    int st = setup_bf16(a, &p, &M);
+    if (st != PU_OK) return st;
+    choose_tile_b(M, a->n, bm, bn);
+    int ks, tp;
+    plan_split_b(a, M, *bm, *bn, &ks, &tp);
+    if (ksplit) *ksplit = (ks > 1 && a->workspace && a->ws_bytes >= (size_t)ks * M * a->n * sizeof(float)) ? ks : 1;
+    return PU_OK;
+}

@@ -708,6 +708,280 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     return PU_OK;
 }
 
+// ------------------------------------------------------------------ bf16 weight gradient (C3)
+// dW[n][k] = sum_m P[m][n] * Q[m][k] with bf16 P (dZ or ConvT input rows) and bf16 im2col Q,
+// fp32 MFMA accumulation (v_mfma_f32_32x32x16_bf16), fp32 slab partials, the same fp64 split
+// reduction.  The GEMM's k dimension is the pixel index m, so each MFMA operand lane needs 8
+// consecutive pixel rows of one column: the stage images are row-major [32 pixel rows][128]
+// bf16 (256-byte rows) read with ds_read_b64_tr_b16 (per 16-lane group: 4 rows x 16 columns,
+// delivered column-major).  The 16-byte chunk ch of row r is stored at ch ^ sw(r),
+// sw(r) = ((r&3)<<2) | ((r>>2)&3) (conflict-free transposed reads on 256-byte rows); glds cannot
+// permute its LDS writes, so each lane fetches the global chunk that belongs at its position.
+typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
+typedef short wi16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) wi16x4 lds_i16x4_t;
+__device__ __attribute__((aligned(16))) __bf16 g_wg_zero_b16[8];
+
+constexpr int WB_ROWS = 32;   // pixel rows per stage (2 MFMA k-steps)
+constexpr int WB_W = 128;     // columns per image (BN = BK = 128)
+
+__device__ __forceinline__ int wb_sw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+struct WgradBf16Params {
+    int M, N, K, Kcp, Nr, C, c0, c1;
+    int Hi, Wi, Ho, Wo, kw, stride, pad;
+    const __bf16* P;
+    const __bf16* src0;
+    const __bf16* src1;
+    int bias_mode;
+    float* slab;
+    int mps, gx, gy;
+    FastDiv dWo, dHo, dC, dKw;
+};
+
+__global__ __launch_bounds__(256) void wgrad_bf16_kernel(const WgradBf16Params p) {
+    constexpr int NBUF = 3;
+    constexpr int LD = WB_ROWS * WB_W * 2 / 1024 / 4;   // glds per wave per image per stage (2)
+    constexpr int G = 2 * LD;
+    constexpr int IMG = WB_ROWS * WB_W;                 // bf16 elements per image
+    constexpr int STAGE = 2 * IMG;
+    __shared__ __attribute__((aligned(16))) __bf16 lds[NBUF * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave & 1, wk = wave >> 1;            // 2 x 2 waves, 64 x 64 each
+    const int lr = lane & 31, lh = lane >> 5;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % p.gx;
+    const int tyz = tile / p.gx;
+    const int ty = tyz % p.gy;
+    const int tz = tyz / p.gy;
+    const int n_blk = ty * WB_W;
+    const int k_blk = tx * WB_W;
+    const int m_begin = tz * p.mps;
+    const int m_end = min(p.M, m_begin + p.mps);
+
+    // loader geometry: instruction j (= wave*LD + jj) of an image covers rows 4j .. 4j+3; lane l
+    // writes physical chunk l%16 of row 4j + l/16, i.e. logical chunk (l%16) ^ sw(row)
+    const int lrow = lane >> 4;                          // row within the instruction
+    int p_col[LD], q_r[LD], q_s[LD], q_cs[LD];
+    const __bf16* q_ptr[LD];
+    bool p_in[LD];
+#pragma unroll
+    for (int jj = 0; jj < LD; ++jj) {
+        const int j = wave * LD + jj;
+        const int ch = (lane & 15) ^ ((lrow << 2) | (j & 3));
+        p_col[jj] = n_blk + 8 * ch;
+        p_in[jj] = p_col[jj] < p.N;
+        const int qk = k_blk + 8 * ch;
+        q_r[jj] = 0; q_s[jj] = 0; q_cs[jj] = 0; q_ptr[jj] = nullptr;
+        if (qk < p.K) {
+            const int tap = fdiv(qk, p.dC);
+            const int c = qk - tap * p.C;
+            q_r[jj] = fdiv(tap, p.dKw);
+            q_s[jj] = tap - q_r[jj] * p.kw;
+            const bool first = c < p.c0;
+            q_ptr[jj] = first ? p.src0 + c : p.src1 + (c - p.c0);
+            q_cs[jj] = first ? p.c0 : p.c1;
+        }
+    }
+
+    auto issue = [&](int m0, int slot) {
+        __bf16* ps = lds + slot * STAGE;
+        __bf16* qs = ps + IMG;
+#pragma unroll
+        for (int jj = 0; jj < LD; ++jj) {
+            const int j = wave * LD + jj;
+            const int m = m0 + 4 * j + lrow;
+            const __bf16* g = g_wg_zero_b16;
+            if (m < m_end && p_in[jj]) g = p.P + (long long)m * p.N + p_col[jj];
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(ps + j * 512), 16, 0, 0);
+        }
+#pragma unroll
+        for (int jj = 0; jj < LD; ++jj) {
+            const int j = wave * LD + jj;
+            const int mu = m0 + 4 * j;                   // wave-uniform
+            const int tu = fdiv(mu, p.dWo);
+            const int wou = mu - tu * p.Wo;
+            const int bu = fdiv(tu, p.dHo);
+            const int hou = tu - bu * p.Ho;
+            int wo = wou + lrow;
+            const int cw = fdiv(wo, p.dWo);
+            wo -= cw * p.Wo;
+            int ho = hou + cw;
+            const int chh = fdiv(ho, p.dHo);
+            ho -= chh * p.Ho;
+            const int b = bu + chh;
+            const __bf16* g = g_wg_zero_b16;
+            if (mu + lrow < m_end && q_ptr[jj]) {
+                const int hi = ho * p.stride - p.pad + q_r[jj], wi = wo * p.stride - p.pad + q_s[jj];
+                if ((unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
+                    g = q_ptr[jj] + ((long long)b * p.Hi * p.Wi + (long long)hi * p.Wi + wi) * q_cs[jj];
+            }
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(qs + j * 512), 16, 0, 0);
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // transposed-read addressing: 16-lane group g = lane>>4 covers columns 16*(g&1) + 0..15 and
+    // rows 8*(g>>1) + (0..3 | 4..7) of a k-step; lane 4q+p of the group addresses row q, columns
+    // 4p..4p+3 (logical chunk (p>>1), byte half (p&1))
+    const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
+    auto tr_addr = [&](int row, int col) {   // byte offset of (row, col) in a swizzled image
+        return row * (WB_W * 2) + 16 * ((col >> 3) ^ wb_sw(row)) + 2 * (col & 7);
+    };
+    const int T = (m_end > m_begin) ? (m_end - m_begin + WB_ROWS - 1) / WB_ROWS : 0;
+    const int bias_w = (p.bias_mode == 1 && tx == 0) ? 1 : (p.bias_mode == 2 && ty == 0) ? 2 : 0;
+    float bsum = 0.f;
+
+#pragma unroll
+    for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(m_begin + s0 * WB_ROWS, s0);
+
+    for (int t = 0; t < T; ++t) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        __builtin_amdgcn_s_barrier();
+        const char* pb = reinterpret_cast<const char*>(lds + (t % NBUF) * STAGE);
+        const char* qb = pb + IMG * 2;
+        wbf16x8 fa[2][2], fb[2][2];   // [kstep][frag]
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int row0 = ks * 16 + 8 * (grp >> 1) + gq;
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const int ccol = 16 * (grp & 1) + 4 * gp;
+                // A operand: Q^T rows = k columns of the Q image
+                const int qc = wk * 64 + f * 32 + ccol;
+                const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(qb + tr_addr(row0, qc)));
+                const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(qb + tr_addr(row0 + 4, qc)));
+                // B operand: P columns n
+                const int pc = wn * 64 + f * 32 + ccol;
+                const wi16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(pb + tr_addr(row0, pc)));
+                const wi16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(pb + tr_addr(row0 + 4, pc)));
+                typedef short wi16x8 __attribute__((ext_vector_type(8)));
+                const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const wi16x8 bv = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                fa[ks][f] = __builtin_bit_cast(wbf16x8, av);
+                fb[ks][f] = __builtin_bit_cast(wbf16x8, bv);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+            if (ks == 0) issue(m_begin + (t + NBUF - 1) * WB_ROWS, (t + NBUF - 1) % NBUF);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        if (bias_w && tid < WB_W) {           // bias column sums: P columns (mode 1) / Q (mode 2)
+            const char* img = bias_w == 1 ? pb : qb;
+            for (int r = 0; r < WB_ROWS; ++r)
+                bsum += (float)*reinterpret_cast<const __bf16*>(img + tr_addr(r, tid));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
+    if (bias_w && tid < WB_W) {
+        if (bias_w == 1) {
+            const int n = n_blk + tid;
+            if (n < p.N) slab[(long long)n * p.Kcp + p.K] = bsum;
+        } else {
+            const int k = k_blk + tid;
+            if (k < p.K) slab[(long long)p.N * p.Kcp + k] = bsum;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = n_blk + wn * 64 + j * 32 + lr;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = k_blk + wk * 64 + i * 32 + 8 * q + 4 * lh;
+                if (k >= p.K) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
+            }
+    }
+}
+
+// phase 2 of every weight-gradient path: fixed-order fp64 reduction of the split partials and
+// the scatter into PyTorch's [n][c][kh][kw] (+ bias)
+static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* workspace, hipStream_t s) {
+    const long long total = (long long)pl.Nr * pl.Kcp;
+    const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
+    const dim3 fgrid((unsigned)((threads + 255) / 256));
+    if (pl.G == 1) {
+        hipLaunchKernelGGL(wgrad_finish_kernel<float>, fgrid, dim3(256), 0, s, (const float*)workspace, pl.splits,
+                           pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,
+                           a->accumulate);
+    } else {
+        double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
+        hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
+                           (const float*)workspace, pl.splits, total, pl.G, part);
+        hipLaunchKernelGGL(wgrad_finish_kernel<double>, fgrid, dim3(256), 0, s, (const double*)part, pl.G, pl.Nr,
+                           pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,
+                           a->accumulate);
+    }
+    return check_launch("pu_wgrad (reduce)");
+}
+
+static void plan_groups(WgradPlan* pl) {
+    const long long total = (long long)pl->Nr * pl->Kcp;
+    int G = (int)ceil_div(262144LL, total);
+    const int by_len = ceil_div(pl->splits, 8);
+    if (G > by_len) G = by_len;
+    if (G > 16) G = 16;
+    pl->G = G < 1 ? 1 : G;
+}
+
+// bf16 plan: 128 x 128 tiles of the N x K GEMM (bias via LDS column sums), pixel rows split so
+// that one round of resident blocks (3 per CU: 48 KB ring) fills the chip
+static int plan_wgrad_bf16(const pu_wgrad_args* a, WgradPlan* pl) {
+    PU_REQUIRE(a && a->batch > 0 && a->out_h > 0 && a->out_w > 0 && a->in_h > 0 && a->in_w > 0, "pu_wgrad_bf16: bad grid");
+    PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0, "pu_wgrad_bf16: bad taps");
+    PU_REQUIRE(a->rows && a->n > 0 && a->src0 && a->c0 > 0 && (a->c1 == 0 || a->src1), "pu_wgrad_bf16: operands");
+    PU_REQUIRE(a->n % 8 == 0 && a->c0 % 8 == 0 && a->c1 % 8 == 0,
+               "pu_wgrad_bf16: n (%d) and channel counts (%d, %d) must be multiples of 8", a->n, a->c0, a->c1);
+    PU_REQUIRE(a->bias_mode >= 0 && a->bias_mode <= 2 && (a->bias_mode == 0 || a->dbias) && a->dweight, "pu_wgrad_bf16: outputs");
+    PU_REQUIRE((((uintptr_t)a->rows | (uintptr_t)a->src0 | (uintptr_t)a->src1) & 15) == 0, "pu_wgrad_bf16: 16-byte alignment");
+    const long long M = (long long)a->batch * a->out_h * a->out_w;
+    PU_REQUIRE(M < (1LL << 31), "pu_wgrad_bf16: too many pixels");
+    pl->M = (int)M;
+    pl->C = a->c0 + a->c1;
+    pl->K = a->kh * a->kw * pl->C;
+    pl->Nr = a->n + (a->bias_mode == 2 ? 1 : 0);
+    pl->Kc = pl->K + (a->bias_mode == 1 ? 1 : 0);
+    pl->Kcp = (pl->Kc + 3) / 4 * 4;
+    pl->qvec = true; pl->dma = true; pl->small = false;
+    pl->BN = WB_W; pl->BK = WB_W;
+    pl->gx = ceil_div(pl->K, WB_W);
+    pl->gy = ceil_div(a->n, WB_W);
+    const int tiles = pl->gx * pl->gy;
+    int splits = 768 / tiles;
+    const int max_splits = ceil_div(M, 512);
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    pl->mps = ceil_div(ceil_div(M, splits), WB_ROWS) * WB_ROWS;
+    pl->splits = ceil_div(M, pl->mps);
+    plan_groups(pl);
+    return PU_OK;
+}
+
 }  // namespace pu
 
 using namespace pu;
@@ -791,21 +1065,42 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
         if (st != PU_OK) return st;
     }
     if (!(phase & 2)) return PU_OK;
+    return wgrad_reduce(pl, a, workspace, s);
+}
 
-    const long long total = (long long)pl.Nr * pl.Kcp;
-    const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
-    const dim3 fgrid((unsigned)((threads + 255) / 256));
-    if (pl.G == 1) {
-        hipLaunchKernelGGL(wgrad_finish_kernel<float>, fgrid, dim3(256), 0, s, (const float*)workspace, pl.splits,
-                           pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,
-                           a->accumulate);
-    } else {
-        double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
-        hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
-                           (const float*)workspace, pl.splits, total, pl.G, part);
-        hipLaunchKernelGGL(wgrad_finish_kernel<double>, fgrid, dim3(256), 0, s, (const double*)part, pl.G, pl.Nr,
-                           pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,
-                           a->accumulate);
+extern "C" size_t pu_wgrad_bf16_workspace_bytes(const pu_wgrad_args* a) {
+    WgradPlan pl;
+    if (plan_wgrad_bf16(a, &pl) != PU_OK) return 0;
+    return pl.ws_bytes();
+}
+
+extern "C" int pu_wgrad_bf16_phase(const pu_wgrad_args* a, void* workspace, size_t ws_bytes, int phase, void* stream) {
+    PU_REQUIRE(phase >= 1 && phase <= 3, "pu_wgrad_bf16_phase: phase %d", phase);
+    WgradPlan pl;
+    int st = plan_wgrad_bf16(a, &pl);
+    if (st != PU_OK) return st;
+    const size_t need = pl.ws_bytes();
+    if (!workspace || ws_bytes < need)
+        return fail(PU_ERR_WORKSPACE, "pu_wgrad_bf16: workspace %zu < %zu bytes", ws_bytes, need);
+    hipStream_t s = as_stream(stream);
+    if (phase & 1) {
+        WgradBf16Params p;
+        p.M = pl.M; p.N = a->n; p.K = pl.K; p.Kcp = pl.Kcp; p.Nr = pl.Nr; p.C = pl.C; p.c0 = a->c0; p.c1 = a->c1;
+        p.Hi = a->in_h; p.Wi = a->in_w; p.Ho = a->out_h; p.Wo = a->out_w;
+        p.kw = a->kw; p.stride = a->stride; p.pad = a->pad;
+        p.P = (const __bf16*)a->rows; p.src0 = (const __bf16*)a->src0; p.src1 = (const __bf16*)a->src1;
+        p.bias_mode = a->bias_mode;
+        p.slab = (float*)workspace; p.mps = pl.mps; p.gx = pl.gx; p.gy = pl.gy;
+        p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
+        p.dC = make_fastdiv(pl.C); p.dKw = make_fastdiv(a->kw);
+        hipLaunchKernelGGL(wgrad_bf16_kernel, dim3(pl.gx * pl.gy * pl.splits), dim3(256), 0, s, p);
+        st = check_launch("pu_wgrad_bf16 (gemm)");
+        if (st != PU_OK) return st;
     }
-    return check_launch("pu_wgrad (reduce)");
+    if (!(phase & 2)) return PU_OK;
+    return wgrad_reduce(pl, a, workspace, s);
+}
+
+extern "C" int pu_wgrad_bf16(const pu_wgrad_args* a, void* workspace, size_t ws_bytes, void* stream) {
+    return pu_wgrad_bf16_phase(a, workspace, ws_bytes, 3, stream);
 }

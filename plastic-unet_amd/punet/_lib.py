@@ -70,6 +70,20 @@ SIGNATURES = [
     ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_nchw_to_nhwc", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_channel_scale", c_int, [P, P, P, c_int, c_ll, c_int, P]),
+    ("pu_conv_igemm_bf16", c_int, [ctypes.POINTER(ConvArgs), P]),
+    ("pu_conv_igemm_bf16_workspace_bytes", c_size, [ctypes.POINTER(ConvArgs)]),
+    ("pu_conv_igemm_bf16_tile", c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                        ctypes.POINTER(c_int)]),
+    ("pu_wgrad_bf16_workspace_bytes", c_size, [ctypes.POINTER(WgradArgs)]),
+    ("pu_wgrad_bf16", c_int, [ctypes.POINTER(WgradArgs), P, c_size, P]),
+    ("pu_wgrad_bf16_phase", c_int, [ctypes.POINTER(WgradArgs), P, c_size, c_int, P]),
+    ("pu_pack_weight_bf16", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    ("pu_convert_f32_bf16", c_int, [P, P, c_ll, P]),
+    ("pu_convert_bf16_f32", c_int, [P, P, c_ll, P]),
+    ("pu_maxpool2_fwd_bf16", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    ("pu_maxpool2_bwd_bf16", c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    ("pu_outconv_fwd_bf16", c_int, [P, P, P, P, c_ll, c_int, P]),
+    ("pu_outconv_bwd_bf16", c_int, [P, P, P, P, P, P, c_ll, c_int, c_int, P, c_size, P]),
     ("pu_add_coords", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_column_sum_workspace_bytes", c_size, [c_ll, c_int]),
     ("pu_column_sum", c_int, [P, c_ll, c_int, P, c_int, P, c_size, P]),

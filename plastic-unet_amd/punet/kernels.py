@@ -87,16 +87,24 @@ def round16(k):
     return (k + 15) // 16 * 16
 
 
-def _req(t, name):
+def _req(t, name, dtype=torch.float32):
     if t is None:
         return
     if not t.is_cuda:
         raise RuntimeError("%s must be on the ROCm device (got %s); the plastic U-Net path has no CPU "
                            "fallback" % (name, t.device))
-    if t.dtype != torch.float32:
-        raise RuntimeError("%s must be float32 (got %s)" % (name, t.dtype))
+    if t.dtype != dtype:
+        raise RuntimeError("%s must be %s (got %s)" % (name, dtype, t.dtype))
     if not t.is_contiguous():
         raise RuntimeError("%s must be contiguous" % name)
+
+
+BF16 = torch.bfloat16
+
+
+def _act_dtype(t):
+    """Activation dtype of a call: float32, or bfloat16 for the bf16 (C3) entry points."""
+    return BF16 if t.dtype == BF16 else torch.float32
 
 
 def device_info(device=0):
@@ -120,9 +128,11 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
           shuffle=False, cgroup=0, resid=None, shuf=(0, 0, 0)):
     """pu_conv_igemm: implicit-GEMM conv (3x3 fwd/dgrad, ConvT fwd with shuffle, ConvT dgrad).
     resid: residual tensor added before ReLU/mask; shuf = (out_h, out_w, crop) of a SHUFFLE2 grid."""
-    for t, nm in ((src0, "src0"), (src1, "src1"), (weight, "weight"), (bias, "bias"), (dst0, "dst0"),
+    dt = _act_dtype(src0)
+    for t, nm in ((src0, "src0"), (src1, "src1"), (weight, "weight"), (dst0, "dst0"),
                   (dst1, "dst1"), (mask0, "mask0"), (mask1, "mask1"), (resid, "resid")):
-        _req(t, nm)
+        _req(t, nm, dt)
+    _req(bias, "bias")
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
         | (PU_EPI_RESID if resid is not None else 0)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
@@ -130,6 +140,9 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,
                  _p(resid), shuf[0], shuf[1], shuf[2])
     L = lib()
+    if dt == BF16:
+        _igemm_bf16(L, a, batch, out_hw, k, c0, c1, n, dst0)
+        return
     nbytes = L.pu_conv_igemm_workspace_bytes(ctypes.byref(a))
     if nbytes:     # split-K scratch from the caching allocator (stream-ordered reuse)
         ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=dst0.device)
@@ -155,15 +168,46 @@ def n0_mask(n, n0, mask0, mask1):
     return (n0 if mask0 is not None else 0) + (n - n0 if mask1 is not None else 0)
 
 
+def _igemm_bf16(L, a, batch, out_hw, k, c0, c1, n, dst0):
+    nbytes = L.pu_conv_igemm_bf16_workspace_bytes(ctypes.byref(a))
+    if nbytes:
+        ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=dst0.device)
+        a.workspace, a.ws_bytes = ws.data_ptr(), nbytes
+    if _PROF is None:
+        check(L.pu_conv_igemm_bf16(ctypes.byref(a), _stream()), "pu_conv_igemm_bf16")
+        return
+    bm, bn, ks = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    L.pu_conv_igemm_bf16_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(ks))
+    M = batch * out_hw[0] * out_hw[1]
+    tag = "igemm_bf16<%dx%d%s>" % (bm.value, bn.value, ",k%d" % ks.value if ks.value > 1 else "")
+    with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
+        check(L.pu_conv_igemm_bf16(ctypes.byref(a), _stream()), "pu_conv_igemm_bf16")
+
+
 def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, src1=None, c1=0,
           bias_mode=0, dbias=None, accumulate=False):
-    """pu_wgrad: split-K weight (+bias) gradient into PyTorch's [n][c][k][k] layout."""
-    for t, nm in ((rows, "rows"), (src0, "src0"), (src1, "src1"), (dweight, "dweight"), (dbias, "dbias")):
-        _req(t, nm)
+    """pu_wgrad: split-K weight (+bias) gradient into PyTorch's [n][c][k][k] layout (fp32, or
+    bf16 rows/sources with fp32 gradients)."""
+    dt = _act_dtype(rows)
+    for t, nm in ((rows, "rows"), (src0, "src0"), (src1, "src1")):
+        _req(t, nm, dt)
+    _req(dweight, "dweight"); _req(dbias, "dbias")
     a = WgradArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                   _p(rows), n, _p(src0), c0, _p(src1), c1, bias_mode, _p(dweight), _p(dbias),
                   1 if accumulate else 0)
     L = lib()
+    if dt == BF16:
+        nbytes = L.pu_wgrad_bf16_workspace_bytes(ctypes.byref(a))
+        ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=rows.device)
+        if nbytes == 0 or _PROF is None:
+            check(L.pu_wgrad_bf16(ctypes.byref(a), ws.data_ptr(), nbytes, _stream()), "pu_wgrad_bf16")
+            return
+        M = batch * out_hw[0] * out_hw[1]
+        with _Rec("wgrad_bf16<128x128>", flops=2.0 * M * n * k * k * (c0 + c1)):
+            check(L.pu_wgrad_bf16_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 1, _stream()), "pu_wgrad_bf16")
+        with _Rec("wgrad_reduce", nbytes=float(nbytes)):
+            check(L.pu_wgrad_bf16_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 2, _stream()), "pu_wgrad_bf16")
+        return
     nbytes = L.pu_wgrad_workspace_bytes(ctypes.byref(a))
     if nbytes == 0:
         check(L.pu_wgrad(ctypes.byref(a), None, 0, _stream()), "pu_wgrad")
@@ -182,17 +226,34 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
         check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 2, _stream()), "pu_wgrad_phase")
 
 
-def pack_weight(w, mode, k_pad, out=None, cgroup=0):
+def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
+    """Pack an fp32 parameter into a GEMM operand (fp32, or bf16 for the C3 kernels)."""
     _req(w, "w")
     d0, d1, kh, kw = w.shape
     taps = kh * kw
     rows = {0: d0, 1: d1, 2: taps * d1, 3: d0, 4: 4 * d1}[mode]
     if out is None:
-        out = torch.empty(rows, k_pad, dtype=torch.float32, device=w.device)
-    with _Rec("pack_weight", nbytes=4.0 * (w.numel() + out.numel())):
-        check(lib().pu_pack_weight(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, cgroup, _stream()),
-              "pu_pack_weight")
+        out = torch.empty(rows, k_pad, dtype=dtype, device=w.device)
+    fn = lib().pu_pack_weight_bf16 if out.dtype == BF16 else lib().pu_pack_weight
+    with _Rec("pack_weight", nbytes=4.0 * w.numel() + out.element_size() * out.numel()):
+        check(fn(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, cgroup, _stream()), "pu_pack_weight")
     return out
+
+
+def to_bf16(x):
+    _req(x, "x")
+    y = torch.empty(x.shape, dtype=BF16, device=x.device)
+    with _Rec("convert", nbytes=6.0 * x.numel()):
+        check(lib().pu_convert_f32_bf16(x.data_ptr(), y.data_ptr(), x.numel(), _stream()), "pu_convert_f32_bf16")
+    return y
+
+
+def to_f32(x):
+    _req(x, "x", BF16)
+    y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    with _Rec("convert", nbytes=6.0 * x.numel()):
+        check(lib().pu_convert_bf16_f32(x.data_ptr(), y.data_ptr(), x.numel(), _stream()), "pu_convert_bf16_f32")
+    return y
 
 
 def nchw_to_nhwc(x):
@@ -240,36 +301,42 @@ def column_sum(x2d, out=None, accumulate=False):
 
 
 def maxpool2_fwd(x):
-    _req(x, "x")
+    dt = _act_dtype(x)
+    _req(x, "x", dt)
     B, H, W, C = x.shape
-    y = torch.empty(B, H // 2, W // 2, C, dtype=torch.float32, device=x.device)
-    with _Rec("maxpool_fwd", nbytes=4.0 * (x.numel() + y.numel())):
-        check(lib().pu_maxpool2_fwd(x.data_ptr(), y.data_ptr(), B, H, W, C, _stream()), "pu_maxpool2_fwd")
+    y = torch.empty(B, H // 2, W // 2, C, dtype=dt, device=x.device)
+    fn = lib().pu_maxpool2_fwd_bf16 if dt == BF16 else lib().pu_maxpool2_fwd
+    with _Rec("maxpool_fwd", nbytes=x.element_size() * (x.numel() + y.numel())):
+        check(fn(x.data_ptr(), y.data_ptr(), B, H, W, C, _stream()), "pu_maxpool2_fwd")
     return y
 
 
 def maxpool2_bwd(x, dy, dx, relu_mask=True, accumulate=True):
-    _req(x, "x"); _req(dy, "dy"); _req(dx, "dx")
+    dt = _act_dtype(x)
+    _req(x, "x", dt); _req(dy, "dy", dt); _req(dx, "dx", dt)
     B, H, W, C = x.shape
-    with _Rec("maxpool_bwd", nbytes=4.0 * (x.numel() * (3 if accumulate else 2) + dy.numel())):
-        check(lib().pu_maxpool2_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C, int(relu_mask),
-                                    int(accumulate), _stream()), "pu_maxpool2_bwd")
+    fn = lib().pu_maxpool2_bwd_bf16 if dt == BF16 else lib().pu_maxpool2_bwd
+    with _Rec("maxpool_bwd", nbytes=x.element_size() * (x.numel() * (3 if accumulate else 2) + dy.numel())):
+        check(fn(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C, int(relu_mask), int(accumulate), _stream()),
+              "pu_maxpool2_bwd")
     return dx
 
 
 def outconv_fwd(x, w, b):
     """x [B,H,W,C] NHWC, w [C] (flattened [1,C,1,1]), b [1] -> logits [B,H,W]."""
-    _req(x, "x"); _req(w, "w"); _req(b, "b")
+    dt = _act_dtype(x)
+    _req(x, "x", dt); _req(w, "w"); _req(b, "b")
     B, H, W, C = x.shape
     y = torch.empty(B, H, W, dtype=torch.float32, device=x.device)
-    with _Rec("outconv_fwd", nbytes=4.0 * (x.numel() + y.numel())):
-        check(lib().pu_outconv_fwd(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), B * H * W, C, _stream()),
-              "pu_outconv_fwd")
+    fn = lib().pu_outconv_fwd_bf16 if dt == BF16 else lib().pu_outconv_fwd
+    with _Rec("outconv_fwd", nbytes=x.element_size() * x.numel() + 4.0 * y.numel()):
+        check(fn(x.data_ptr(), w.data_ptr(), _p(b), y.data_ptr(), B * H * W, C, _stream()), "pu_outconv_fwd")
     return y
 
 
 def outconv_bwd(x, w, dy, relu_mask=True, out=None):
-    _req(x, "x"); _req(w, "w"); _req(dy, "dy")
+    dt = _act_dtype(x)
+    _req(x, "x", dt); _req(w, "w"); _req(dy, "dy")
     B, H, W, C = x.shape
     rows = B * H * W
     dx = torch.empty_like(x)
@@ -281,9 +348,10 @@ def outconv_bwd(x, w, dy, relu_mask=True, out=None):
     L = lib()
     nbytes = L.pu_outconv_workspace_bytes(rows, C)
     ws = torch.empty(nbytes // 4 + 1, dtype=torch.float32, device=x.device)
-    with _Rec("outconv_bwd", nbytes=4.0 * (2 * x.numel() + rows)):
-        check(L.pu_outconv_bwd(x.data_ptr(), w.data_ptr(), dy.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(),
-                               rows, C, int(relu_mask), ws.data_ptr(), nbytes, _stream()), "pu_outconv_bwd")
+    fn = L.pu_outconv_bwd_bf16 if dt == BF16 else L.pu_outconv_bwd
+    with _Rec("outconv_bwd", nbytes=x.element_size() * 2.0 * x.numel() + 4.0 * rows):
+        check(fn(x.data_ptr(), w.data_ptr(), dy.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                 rows, C, int(relu_mask), ws.data_ptr(), nbytes, _stream()), "pu_outconv_bwd")
     return dx, dw, db
 
 

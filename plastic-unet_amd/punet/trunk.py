@@ -30,16 +30,30 @@ class _Packs:
     def __init__(self):
         self.cache = {}
 
-    def get(self, w, mode, k_pad, cgroup=0):
+    def get(self, w, mode, k_pad, cgroup=0, dtype=torch.float32):
         # keyed by storage (detached views share the parameter's version counter)
-        key = (w.data_ptr(), tuple(w.shape), mode, cgroup)
+        key = (w.data_ptr(), tuple(w.shape), mode, cgroup, dtype)
         ver = w._version
         hit = self.cache.get(key)
         if hit is not None and hit[0] == ver:
             return hit[1]
-        packed = K.pack_weight(w.detach(), mode, k_pad, cgroup=cgroup)
+        packed = K.pack_weight(w.detach(), mode, k_pad, cgroup=cgroup, dtype=dtype)
         self.cache[key] = (ver, packed)
         return packed
+
+
+def _kp(k, dt):
+    """K padded to the kernel's stage: 16 fp32 or 32 bf16 values."""
+    return K.round16(k) if dt == torch.float32 else (k + 31) // 32 * 32
+
+
+def _cg(dt, c0, c1=0):
+    """K order of a packed operand: the fp32 kernels' 16/32-channel groups, or 32 for bf16."""
+    if dt == torch.float32:
+        return K.cgroup_for(c0, c1)
+    if c0 % 32 or c1 % 32:
+        raise RuntimeError("bf16 convolutions need channel counts that are multiples of 32 (got %d, %d)" % (c0, c1))
+    return 32
 
 
 def conv3x3(x0, w, b, packs, x1=None, relu=True):
@@ -47,11 +61,12 @@ def conv3x3(x0, w, b, packs, x1=None, relu=True):
     B, H, W, c0 = x0.shape
     c1 = 0 if x1 is None else x1.shape[3]
     cout = w.shape[0]
-    k_pad = K.round16(9 * (c0 + c1))
-    g = K.cgroup_for(c0, c1)
-    out = torch.empty(B, H, W, cout, dtype=torch.float32, device=x0.device)
+    dt = x0.dtype
+    k_pad = _kp(9 * (c0 + c1), dt)
+    g = _cg(dt, c0, c1)
+    out = torch.empty(B, H, W, cout, dtype=dt, device=x0.device)
     K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=x0, c0=c0, src1=x1, c1=c1,
-            weight=packs.get(w, PU_PACK_CONV_FWD, k_pad, g), k_pad=k_pad, n=cout, bias=b, dst0=out, relu=relu,
+            weight=packs.get(w, PU_PACK_CONV_FWD, k_pad, g, dt), k_pad=k_pad, n=cout, bias=b, dst0=out, relu=relu,
             cgroup=g)
     return out
 
@@ -60,13 +75,14 @@ def conv3x3_dgrad(dz, w, packs, split=None, mask0=None, mask1=None):
     """dX = conv(dZ, flipped W^T); optional channel split [0,split) -> d0, rest -> d1 and masks."""
     B, H, W, cout = dz.shape
     cin = w.shape[1]
-    k_pad = K.round16(9 * cout)
-    g = K.cgroup_for(cout)
+    dt = dz.dtype
+    k_pad = _kp(9 * cout, dt)
+    g = _cg(dt, cout)
     n0 = cin if split is None else split
-    d0 = torch.empty(B, H, W, n0, dtype=torch.float32, device=dz.device)
-    d1 = None if split is None else torch.empty(B, H, W, cin - n0, dtype=torch.float32, device=dz.device)
+    d0 = torch.empty(B, H, W, n0, dtype=dt, device=dz.device)
+    d1 = None if split is None else torch.empty(B, H, W, cin - n0, dtype=dt, device=dz.device)
     K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=dz, c0=cout,
-            weight=packs.get(w, PU_PACK_CONV_DGRAD, k_pad, g), k_pad=k_pad, n=cin, dst0=d0, n0=n0, dst1=d1,
+            weight=packs.get(w, PU_PACK_CONV_DGRAD, k_pad, g, dt), k_pad=k_pad, n=cin, dst0=d0, n0=n0, dst1=d1,
             mask0=mask0, mask1=mask1, cgroup=g)
     return d0, d1
 
@@ -89,10 +105,11 @@ def convT2x2(x, w, b, packs):
     """ConvTranspose2d(cin, cout, 2, stride=2): GEMM [B*h*w, cin] x [cin, 4*cout] + pixel shuffle."""
     B, h, wd, cin = x.shape
     cout = w.shape[1]
-    k_pad = K.round16(cin)
-    out = torch.empty(B, 2 * h, 2 * wd, cout, dtype=torch.float32, device=x.device)
+    dt = x.dtype
+    k_pad = _kp(cin, dt)
+    out = torch.empty(B, 2 * h, 2 * wd, cout, dtype=dt, device=x.device)
     K.igemm(batch=B, in_hw=(h, wd), out_hw=(h, wd), k=1, stride=1, pad=0, src0=x, c0=cin,
-            weight=packs.get(w, PU_PACK_CONVT_FWD, k_pad), k_pad=k_pad, n=4 * cout, bias=b, dst0=out,
+            weight=packs.get(w, PU_PACK_CONVT_FWD, k_pad, 0, dt), k_pad=k_pad, n=4 * cout, bias=b, dst0=out,
             shuffle=True)
     return out
 
@@ -101,11 +118,13 @@ def convT2x2_dgrad(du, w, packs, mask):
     """dX[b,h,w,:] = sum_(i,j) dU[b,2h+i,2w+j,:] W[:, :, i, j]^T, times (mask > 0)."""
     B, H2, W2, cout = du.shape
     cin = w.shape[0]
-    k_pad = K.round16(4 * cout)
-    g = K.cgroup_for(cout)
-    dx = torch.empty(B, H2 // 2, W2 // 2, cin, dtype=torch.float32, device=du.device)
+    dt = du.dtype
+    k_pad = _kp(4 * cout, dt)
+    g = _cg(dt, cout)
+    dx = torch.empty(B, H2 // 2, W2 // 2, cin, dtype=dt, device=du.device)
     K.igemm(batch=B, in_hw=(H2, W2), out_hw=(H2 // 2, W2 // 2), k=2, stride=2, pad=0, src0=du, c0=cout,
-            weight=packs.get(w, PU_PACK_CONVT_DGRAD, k_pad, g), k_pad=k_pad, n=cin, dst0=dx, mask0=mask, cgroup=g)
+            weight=packs.get(w, PU_PACK_CONVT_DGRAD, k_pad, g, dt), k_pad=k_pad, n=cin, dst0=dx, mask0=mask,
+            cgroup=g)
     return dx
 
 
@@ -140,6 +159,9 @@ class UNetpTrunk:
         self.coord = getattr(model, "coord", None)
         self.with_r = bool(getattr(model, "with_r", False))
         self.up_first = bool(getattr(model, "up_first", False))
+        # activations dtype: float32, or bfloat16 (config C3; fp32 accumulation, fp32 parameters
+        # and gradients; the 1-channel stem conv runs in fp32 and its output is rounded once)
+        self.dtype = getattr(model, "compute_dtype", torch.float32)
         self.names = []
         self.packs = _Packs()
         mods = {"inc": model.inc.conv.conv}
@@ -191,7 +213,10 @@ class UNetpTrunk:
                     weight=pk.get(cw, PU_PACK_CONV_FWD, K.round16(ca)), k_pad=K.round16(ca), n=cw.shape[0],
                     bias=cb, dst0=x, relu=True)
             s["stem"] = x
-        w, b = nxt(); t = conv3x3(x, w, b, pk); s["inc.t"] = t
+        w, b = nxt(); t = conv3x3(x, w, b, pk)
+        if self.dtype != t.dtype:
+            t = K.to_bf16(t)
+        s["inc.t"] = t
         w, b = nxt(); y = conv3x3(t, w, b, pk)
         skips = [y]
         for i in range(1, D):
@@ -283,6 +308,8 @@ class UNetpTrunk:
         grads[2], grads[3] = conv3x3_wgrad(g, t, out=out(2))
         dt, _ = conv3x3_dgrad(g, P[2], pk, mask0=t)
         x0 = s["stem"] if self.coord is not None else s["x"]
+        if dt.dtype != x0.dtype:       # bf16 trunk: the fp32 stem's weight gradient
+            dt = K.to_f32(dt)
         grads[0], grads[1] = conv3x3_wgrad(dt, x0, out=out(0))
         if self.debug is not None:
             self.debug["inc.c0"] = dt

@@ -11,6 +11,9 @@ Extensions (keyword-only in spirit, defaults reproduce the reference):
   depth=5, base_ch=8      generalised trunk width/depth (config C2 = depth 5, base 64)
   forward(x [B,C,N,N], hebb [B,N,N]) batches B independent per-slot traces; with hebb [N,N] the
   reference rule "batch size must be 1" applies unchanged.
+  precision='bf16'        config C3: bf16 activations / packed weights on bf16 MFMA with fp32
+                          accumulation; parameters, gradients, Adam, logits and the plastic head
+                          stay fp32 (base_ch must be a multiple of 32).
 """
 import torch
 import torch.nn as nn
@@ -86,8 +89,14 @@ def _check_gpu_tensor(t, what):
 
 class UNetp(nn.Module):
     def __init__(self, n_channels, n_classes, device, alfa_type='free', rule='hebb', nbf=128, batch_norm=False,
-                 bilinear_upsample=False, depth=5, base_ch=8):
+                 bilinear_upsample=False, depth=5, base_ch=8, precision='fp32'):
         super().__init__()
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if precision == "bf16" and base_ch % 32:
+            raise ValueError("precision='bf16' needs base_ch to be a multiple of 32 (got %d)" % base_ch)
+        self.precision = precision
+        self.compute_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
         self.n_classes = n_classes
         self.n_channels = n_channels
         self.nbf = nbf
