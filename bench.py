@@ -125,29 +125,62 @@ def cpu_baseline(args):
                       % (type(net).__name__, args.img, args.img, n, el, threads)}
 
 
+def _launch_time_us(fn, reps):
+    """Average device time of one fn() launch: `reps` launches captured in a HIP graph and replayed
+    (no Python/ctypes launch overhead between them); eager back-to-back launches if capture fails."""
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(5):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / (5 * reps), "hip_graph"
+    except Exception:
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps, "eager"
+
+
 def oja_update_bench(K, B, N, device):
-    """Algorithmic GB/s of the trace update: 8*B*N^2 + 8*B*N bytes (read H, write H', rows)."""
+    """Algorithmic GB/s of the Oja trace update: 8*B*N^2 + 8*B*N bytes (read H, write H', rows),
+    the stand-alone kernel at the bench batch (cache-resident) and over an HBM-sized sweep; plus
+    the fused head forward (GEMM + sigmoid + Oja update in one launch, 16*B*N^2 + 8*N^2 bytes)."""
     res = {}
     eta = torch.full((1,), 0.01, device=device)
-    sweep = max(1, (1 << 30) // (4 * N * N))            # 1 GiB of traces (8192 at N=128)
-    for label, bb, reps in (("bs%d" % B, B, 200), ("hbm_sweep_%d" % sweep, sweep, 20)):
+    sweep = max(1, (1 << 30) // (4 * N * N))            # 1 GiB of traces (16384 at N=128)
+    for label, bb, reps in (("bs%d" % B, B, 100), ("hbm_sweep_%d" % sweep, sweep, 10)):
         H = torch.randn(bb, N, N, device=device)
         X = torch.randn(bb, N, N, device=device)
         Y = torch.rand(bb, N, N, device=device)
         out = torch.empty_like(H)
-        for _ in range(3):
-            K.trace_update(H, X, Y, eta, 1, out=out)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        e0.record()
-        for _ in range(reps):
-            K.trace_update(H, X, Y, eta, 1, out=out)
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
+        us, how = _launch_time_us(lambda: K.trace_update(H, X, Y, eta, 1, out=out), reps)
         nbytes = 8.0 * bb * N * N + 8.0 * bb * N
-        res[label] = {"us_per_launch": round(us, 3), "bytes": nbytes, "GB_s": round(nbytes / us / 1e3, 1)}
+        res[label] = {"us_per_launch": round(us, 3), "bytes": nbytes, "GB_s": round(nbytes / us / 1e3, 1),
+                      "timing": how}
         del H, X, Y, out
+    H = 0.1 * torch.randn(B, N, N, device=device)
+    X = torch.randn(B, N, N, device=device)
+    w = 0.01 * torch.randn(N, N, device=device)
+    a = 0.01 * torch.rand(N, N, device=device)
+    us, how = _launch_time_us(lambda: K.plastic_fwd(X, H, w, a, eta, 1, True), 50)
+    nbytes = 16.0 * B * N * N + 8.0 * N * N
+    res["fused_head_bs%d" % B] = {"us_per_launch": round(us, 3), "bytes": nbytes,
+                                 "GB_s": round(nbytes / us / 1e3, 1),
+                                 "TFLOP_s": round(2.0 * B * N ** 3 / us / 1e6, 2), "timing": how}
     return res
 
 

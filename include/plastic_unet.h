@@ -236,7 +236,9 @@ int pu_outconv_bwd_bf16(const void* x, const float* w, const float* dy, void* dx
  *   Y_b = sigmoid(X_b (w + alpha (.) H_b))
  *   hebb rule (0): H'_b = (1-eta) H_b + eta x0 y0^T ;  oja rule (1): H'_b = H_b + eta (x0 - H_b y0) y0
  *   with x0 = X_b[0,:], y0 = Y_b[0,:]; hebb_out may be NULL (eval: trace not updated).
- * eta is a device pointer (the learnable parameter).
+ * eta is a device pointer (the learnable parameter).  pu_plastic_fwd is ONE launch when hebb_out
+ * is a separate buffer (the trace update is fused into the GEMM's epilogue); hebb_out == hebb
+ * (in place) takes a second, element-wise launch.  pu_trace_update is the update alone.
  * ------------------------------------------------------------------------------------------- */
 enum { PU_RULE_HEBB = 0, PU_RULE_OJA = 1 };
 

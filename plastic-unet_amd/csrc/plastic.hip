@@ -17,31 +17,51 @@ namespace pu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int HT = 64;   // output tile
-constexpr int HK = 16;   // k chunk
+constexpr int HK = 16;   // k chunk staged through LDS
 
-// Y[b][i][j] = sigmoid( sum_k X[b][i][k] * (w[k][j] + alpha[k][j]*H[b][k][j]) )
-// 256 threads, each a 4x4 micro-tile of the 64x64 block tile.
-__global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict__ X, const float* __restrict__ H,
-                                                        const float* __restrict__ w, const float* __restrict__ alpha,
-                                                        float* __restrict__ Y, int N) {
+// Tile T x T per 256-thread block (T = 64: 4x4 per thread; T = 32: 2x2, for grids that would not
+// fill the chip, e.g. bs 32 x 128^2 -> 512 blocks instead of 128).
+template <int T> struct HeadTile {
+    static constexpr int M = T / 16;   // micro-tile side
+};
+
+__device__ __forceinline__ float trace_rule(float h, float x0, float y0, float eta, float one_m_eta, int rule) {
 #pragma clang fp contract(off)
-    __shared__ float xs[HK][HT + 4];   // xs[k][i]
-    __shared__ float ws[HK][HT + 4];   // ws[k][j]
+    // unet_p.py:82 (Hebb) and :84 (Oja), in the reference's operation order
+    return rule == PU_RULE_HEBB ? one_m_eta * h + eta * (x0 * y0) : h + eta * ((x0 - h * y0) * y0);
+}
+
+// Y[b][i][j] = sigmoid( sum_k X[b][i][k] * (w[k][j] + alpha[k][j]*H[b][k][j]) )     (unet_p.py:70-79)
+// With Hn != nullptr the trace update is fused in: every block also accumulates row 0 of its
+// column tile (y0 = Y[b][0][j0:j0+T], the same fmaf chain as the block that owns row 0, so the
+// values are identical) and then writes H'[b][k][j] for its own T x T tile with k in the tile's
+// row range: H is read from HBM once for Weff and re-read from L2 for the update; one launch.
+// Hn must not alias H (other blocks still read H).  grid (N/T, N/T, B)
+template <int T>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__ X, const float* __restrict__ H,
+                                                       const float* __restrict__ w, const float* __restrict__ alpha,
+                                                       float* __restrict__ Y, float* __restrict__ Hn,
+                                                       const float* __restrict__ eta_p, int N, int rule) {
+#pragma clang fp contract(off)
+    constexpr int M = HeadTile<T>::M;
+    __shared__ float xs[HK][T + 4];    // xs[k][i]
+    __shared__ float ws[HK][T + 4];    // ws[k][j]
+    __shared__ float x0s[HK];          // X[b][0][k]
+    __shared__ float y0s[T];
     const int b = blockIdx.z;
-    const int i0 = blockIdx.y * HT, j0 = blockIdx.x * HT;
+    const int i0 = blockIdx.y * T, j0 = blockIdx.x * T;
     const float* Xb = X + (long long)b * N * N;
     const float* Hb = H + (long long)b * N * N;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    float acc[4][4] = {};
+    const bool fuse = Hn != nullptr;
+    float acc[M][M] = {};
+    float acc0[M] = {};
     for (int k0 = 0; k0 < N; k0 += HK) {
-        for (int e = threadIdx.x; e < HK * HT; e += 256) {
-            // X tile: row i (64) x k (16), stored transposed
-            int kk = e % HK, ii = e / HK;
+        for (int e = threadIdx.x; e < HK * T; e += 256) {
+            int kk = e % HK, ii = e / HK;               // X tile: row i x k, stored transposed
             int gi = i0 + ii, gk = k0 + kk;
             xs[kk][ii] = (gi < N && gk < N) ? Xb[(long long)gi * N + gk] : 0.f;
-            // Weff tile: k (16) x j (64)
-            int jj = e % HT, kk2 = e / HT;
+            int jj = e % T, kk2 = e / T;                // Weff tile: k x j
             int gj = j0 + jj, gk2 = k0 + kk2;
             float v = 0.f;
             if (gj < N && gk2 < N) {
@@ -50,82 +70,86 @@ __global__ __launch_bounds__(256) void head_gemm_kernel(const float* __restrict_
             }
             ws[kk2][jj] = v;
         }
+        if (fuse && threadIdx.x < HK) x0s[threadIdx.x] = (k0 + threadIdx.x < N) ? Xb[k0 + threadIdx.x] : 0.f;
         __syncthreads();
 #pragma unroll
         for (int kk = 0; kk < HK; ++kk) {
-            float a[4], bb[4];
+            float a[M], bb[M];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { a[q] = xs[kk][ty * 4 + q]; bb[q] = ws[kk][tx * 4 + q]; }
+            for (int q = 0; q < M; ++q) { a[q] = xs[kk][ty * M + q]; bb[q] = ws[kk][tx * M + q]; }
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < M; ++q)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[q][r] = fmaf(a[q], bb[r], acc[q][r]);
+                for (int r = 0; r < M; ++r) acc[q][r] = fmaf(a[q], bb[r], acc[q][r]);
+            if (fuse && ty == 0) {
+                const float a0 = x0s[kk];
+#pragma unroll
+                for (int r = 0; r < M; ++r) acc0[r] = fmaf(a0, bb[r], acc0[r]);
+            }
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        int gi = i0 + ty * 4 + q;
+    for (int q = 0; q < M; ++q) {
+        int gi = i0 + ty * M + q;
         if (gi >= N) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            int gj = j0 + tx * 4 + r;
+        for (int r = 0; r < M; ++r) {
+            int gj = j0 + tx * M + r;
             if (gj < N) Y[((long long)b * N + gi) * N + gj] = 1.f / (1.f + expf(-acc[q][r]));
         }
     }
-}
-
-// H'[b][k][j] from x0 = X[b][0][k] and y0 = Y[b][0][j]  (unet_p.py:81-86)
-__global__ void trace_kernel(const float* __restrict__ H, const float* __restrict__ X, const float* __restrict__ Y,
-                             const float* __restrict__ eta_p, float* __restrict__ Hn, int N, long long total, int rule) {
-#pragma clang fp contract(off)
+    if (!fuse) return;
+    if (ty == 0) {
+#pragma unroll
+        for (int r = 0; r < M; ++r) y0s[tx * M + r] = 1.f / (1.f + expf(-acc0[r]));
+    }
+    __syncthreads();
     const float eta = eta_p[0];
     const float one_m_eta = 1.f - eta;
-    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const long long nn = (long long)N * N;
-        const long long b = idx / nn;
-        const int rem = int(idx - b * nn);
-        const int k = rem / N, j = rem - k * N;
-        const float h = H[idx];
-        const float x0 = X[b * nn + k];
-        const float y0 = Y[b * nn + j];
-        float out;
-        if (rule == PU_RULE_HEBB) {
-            out = one_m_eta * h + eta * (x0 * y0);
-        } else {
-            out = h + eta * ((x0 - h * y0) * y0);
+    float* Hnb = Hn + (long long)b * N * N;
+    // H' rows k = i0.. (the tile's row range), columns j0..: coalesced over j
+    for (int e = threadIdx.x; e < T * T; e += 256) {
+        const int kk = e / T, jj = e % T;
+        const int gk = i0 + kk, gj = j0 + jj;
+        if (gk < N && gj < N) {
+            const long long o = (long long)gk * N + gj;
+            Hnb[o] = trace_rule(Hb[o], Xb[gk], y0s[jj], eta, one_m_eta, rule);
         }
-        Hn[idx] = out;
     }
 }
 
-// float4 variant for N % 4 == 0 (the bs=32 x 128^2 Oja update measured in bench.py)
+// H'[b][k][j] from x0 = X[b][0][k] and y0 = Y[b][0][j]  (unet_p.py:81-86); the stand-alone update
+// (pu_trace_update).  grid (ceil(N*N/4 / 256), B): one float4 per thread, 32-bit indexing
+__global__ void trace_kernel(const float* __restrict__ H, const float* __restrict__ X, const float* __restrict__ Y,
+                             const float* __restrict__ eta_p, float* __restrict__ Hn, int N, int rule) {
+#pragma clang fp contract(off)
+    const float eta = eta_p[0];
+    const float one_m_eta = 1.f - eta;
+    const long long off = (long long)blockIdx.y * N * N;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= N * N) return;
+    const int k = idx / N, j = idx - k * N;
+    Hn[off + idx] = trace_rule(H[off + idx], X[off + k], Y[off + j], eta, one_m_eta, rule);
+}
+
 __global__ void trace_kernel_v4(const float* __restrict__ H, const float* __restrict__ X, const float* __restrict__ Y,
-                                const float* __restrict__ eta_p, float* __restrict__ Hn, int N, long long total4,
-                                int rule) {
+                                const float* __restrict__ eta_p, float* __restrict__ Hn, int N, int rule) {
 #pragma clang fp contract(off)
     const float eta = eta_p[0];
     const float one_m_eta = 1.f - eta;
     const int N4 = N >> 2;
-    const long long nn = (long long)N * N;
-    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total4;
-         idx += (long long)gridDim.x * blockDim.x) {
-        const long long row = idx / N4;            // b*N + k
-        const int j4 = int(idx - row * N4);
-        const long long b = row / N;
-        const int k = int(row - b * N);
-        const f32x4 h = reinterpret_cast<const f32x4*>(H)[idx];
-        const float x0 = X[b * nn + k];
-        const f32x4 y0 = *reinterpret_cast<const f32x4*>(Y + b * nn + j4 * 4);
-        f32x4 out;
+    const long long off = (long long)blockIdx.y * N * N;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;    // float4 index within the slot
+    if (idx >= N * N4) return;
+    const int k = idx / N4, j4 = idx - k * N4;
+    const f32x4 h = reinterpret_cast<const f32x4*>(H + off)[idx];
+    const float x0 = X[off + k];
+    const f32x4 y0 = *reinterpret_cast<const f32x4*>(Y + off + j4 * 4);
+    f32x4 out;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if (rule == PU_RULE_HEBB) out[e] = one_m_eta * h[e] + eta * (x0 * y0[e]);
-            else out[e] = h[e] + eta * ((x0 - h[e] * y0[e]) * y0[e]);
-        }
-        reinterpret_cast<f32x4*>(Hn)[idx] = out;
-    }
+    for (int e = 0; e < 4; ++e) out[e] = trace_rule(h[e], x0, y0[e], eta, one_m_eta, rule);
+    reinterpret_cast<f32x4*>(Hn + off)[idx] = out;
 }
 
 // ---------------------------------------------------------------------------------------- backward
@@ -135,20 +159,22 @@ __device__ __forceinline__ float sig_bwd(float dy, float y) {
     return dy * (1.f - y) * y;
 }
 
-// dX[b][i][k] = sum_j G[b][i][j] * Weff_b[k][j]
+// dX[b][i][k] = sum_j G[b][i][j] * Weff_b[k][j]      grid (N/T, N/T, B)
+template <int T>
 __global__ __launch_bounds__(256) void head_dx_kernel(const float* __restrict__ Yv, const float* __restrict__ dY,
                                                       const float* __restrict__ H, const float* __restrict__ w,
                                                       const float* __restrict__ alpha, float* __restrict__ dX, int N) {
 #pragma clang fp contract(off)
-    __shared__ float gs[HK][HT + 4];   // gs[j][i]
-    __shared__ float ws[HK][HT + 4];   // ws[j][k]
+    constexpr int M = HeadTile<T>::M;
+    __shared__ float gs[HK][T + 4];   // gs[j][i]
+    __shared__ float ws[HK][T + 4];   // ws[j][k]
     const int b = blockIdx.z;
-    const int i0 = blockIdx.y * HT, k0 = blockIdx.x * HT;
+    const int i0 = blockIdx.y * T, k0 = blockIdx.x * T;
     const long long off = (long long)b * N * N;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    float acc[4][4] = {};
+    float acc[M][M] = {};
     for (int j0 = 0; j0 < N; j0 += HK) {
-        for (int e = threadIdx.x; e < HK * HT; e += 256) {
+        for (int e = threadIdx.x; e < HK * T; e += 256) {
             int jj = e % HK, rr = e / HK;
             int gj = j0 + jj;
             int gi = i0 + rr;
@@ -169,111 +195,101 @@ __global__ __launch_bounds__(256) void head_dx_kernel(const float* __restrict__ 
         __syncthreads();
 #pragma unroll
         for (int jj = 0; jj < HK; ++jj) {
-            float a[4], bb[4];
+            float a[M], bb[M];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { a[q] = gs[jj][ty * 4 + q]; bb[q] = ws[jj][tx * 4 + q]; }
+            for (int q = 0; q < M; ++q) { a[q] = gs[jj][ty * M + q]; bb[q] = ws[jj][tx * M + q]; }
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < M; ++q)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[q][r] = fmaf(a[q], bb[r], acc[q][r]);
+                for (int r = 0; r < M; ++r) acc[q][r] = fmaf(a[q], bb[r], acc[q][r]);
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        int gi = i0 + ty * 4 + q;
+    for (int q = 0; q < M; ++q) {
+        int gi = i0 + ty * M + q;
         if (gi >= N) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            int gk = k0 + tx * 4 + r;
+        for (int r = 0; r < M; ++r) {
+            int gk = k0 + tx * M + r;
             if (gk < N) dX[off + (long long)gi * N + gk] = acc[q][r];
         }
     }
 }
 
-// T_b[k][j] = sum_i X[b][i][k] * G[b][i][j];  partial[z] = (sum_b T_b, sum_b T_b * H_b) over the
-// block's slot range.  grid (N/64, N/64, bsplit)
+// T_b[k][j] = sum_i X[b][i][k] * G[b][i][j];  per slot: partial[b] = (T_b, T_b * H_b).
+// grid (N/T, N/T, B); the slot sum is a separate fixed-order pass (deterministic)
+template <int T>
 __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ X, const float* __restrict__ Yv,
                                                       const float* __restrict__ dY, const float* __restrict__ H,
-                                                      float* __restrict__ partial, int N, int B, int per) {
+                                                      float* __restrict__ partial, int N) {
 #pragma clang fp contract(off)
-    __shared__ float xs[HK][HT + 4];   // xs[i][k]
-    __shared__ float gs[HK][HT + 4];   // gs[i][j]
-    const int k0 = blockIdx.y * HT, j0 = blockIdx.x * HT;
+    constexpr int M = HeadTile<T>::M;
+    __shared__ float xs[HK][T + 4];   // xs[i][k]
+    __shared__ float gs[HK][T + 4];   // gs[i][j]
+    const int k0 = blockIdx.y * T, j0 = blockIdx.x * T;
+    const int b = blockIdx.z;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    float aw[4][4] = {}, aa[4][4] = {};
-    const int b_begin = blockIdx.z * per, b_end = min(B, b_begin + per);
-    for (int b = b_begin; b < b_end; ++b) {
-        const long long off = (long long)b * N * N;
-        float t[4][4] = {};
-        for (int i0 = 0; i0 < N; i0 += HK) {
-            for (int e = threadIdx.x; e < HK * HT; e += 256) {
-                int cc = e % HT, ii = e / HT;
-                int gi = i0 + ii;
-                int gk = k0 + cc, gj = j0 + cc;
-                xs[ii][cc] = (gi < N && gk < N) ? X[off + (long long)gi * N + gk] : 0.f;
-                float g = 0.f;
-                if (gi < N && gj < N) {
-                    long long o = off + (long long)gi * N + gj;
-                    g = sig_bwd(dY[o], Yv[o]);
-                }
-                gs[ii][cc] = g;
+    const long long off = (long long)b * N * N;
+    float t[M][M] = {};
+    for (int i0 = 0; i0 < N; i0 += HK) {
+        for (int e = threadIdx.x; e < HK * T; e += 256) {
+            int cc = e % T, ii = e / T;
+            int gi = i0 + ii;
+            int gk = k0 + cc, gj = j0 + cc;
+            xs[ii][cc] = (gi < N && gk < N) ? X[off + (long long)gi * N + gk] : 0.f;
+            float g = 0.f;
+            if (gi < N && gj < N) {
+                long long o = off + (long long)gi * N + gj;
+                g = sig_bwd(dY[o], Yv[o]);
             }
-            __syncthreads();
-#pragma unroll
-            for (int ii = 0; ii < HK; ++ii) {
-                float a[4], bb[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) { a[q] = xs[ii][ty * 4 + q]; bb[q] = gs[ii][tx * 4 + q]; }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) t[q][r] = fmaf(a[q], bb[r], t[q][r]);
-            }
-            __syncthreads();
+            gs[ii][cc] = g;
         }
+        __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int gk = k0 + ty * 4 + q;
+        for (int ii = 0; ii < HK; ++ii) {
+            float a[M], bb[M];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int gj = j0 + tx * 4 + r;
-                float h = (gk < N && gj < N) ? H[off + (long long)gk * N + gj] : 0.f;
-                aw[q][r] = aw[q][r] + t[q][r];
-                aa[q][r] = aa[q][r] + t[q][r] * h;
-            }
+            for (int q = 0; q < M; ++q) { a[q] = xs[ii][ty * M + q]; bb[q] = gs[ii][tx * M + q]; }
+#pragma unroll
+            for (int q = 0; q < M; ++q)
+#pragma unroll
+                for (int r = 0; r < M; ++r) t[q][r] = fmaf(a[q], bb[r], t[q][r]);
         }
+        __syncthreads();
     }
-    float* pw = partial + (long long)blockIdx.z * 2 * N * N;
+    float* pw = partial + (long long)b * 2 * N * N;
     float* pa = pw + (long long)N * N;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        int gk = k0 + ty * 4 + q;
+    for (int q = 0; q < M; ++q) {
+        int gk = k0 + ty * M + q;
         if (gk >= N) continue;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            int gj = j0 + tx * 4 + r;
+        for (int r = 0; r < M; ++r) {
+            int gj = j0 + tx * M + r;
             if (gj < N) {
-                pw[(long long)gk * N + gj] = aw[q][r];
-                pa[(long long)gk * N + gj] = aa[q][r];
+                const long long o = (long long)gk * N + gj;
+                pw[o] = t[q][r];
+                pa[o] = t[q][r] * H[off + o];
             }
         }
     }
 }
 
-__global__ void head_dw_reduce_kernel(const float* __restrict__ partial, int nsplit, int N, float* __restrict__ dw,
+// dw = sum_b T_b, dalpha = sum_b T_b * H_b, slots summed in order 0..B-1
+__global__ void head_dw_reduce_kernel(const float* __restrict__ partial, int B, int N, float* __restrict__ dw,
                                       float* __restrict__ da) {
+#pragma clang fp contract(off)
     const long long nn = (long long)N * N;
-    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < nn;
-         idx += (long long)gridDim.x * blockDim.x) {
-        float sw = 0.f, sa = 0.f;
-        for (int z = 0; z < nsplit; ++z) {
-            sw += partial[(long long)z * 2 * nn + idx];
-            sa += partial[(long long)z * 2 * nn + nn + idx];
-        }
-        dw[idx] = sw;
-        da[idx] = sa;
+    const long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (idx >= nn) return;
+    float sw = 0.f, sa = 0.f;
+    for (int z = 0; z < B; ++z) {
+        sw += partial[(long long)z * 2 * nn + idx];
+        sa += partial[(long long)z * 2 * nn + nn + idx];
     }
+    dw[idx] = sw;
+    da[idx] = sa;
 }
 
 // --------------------------------------------------------------------------------------------- BCE
@@ -331,9 +347,25 @@ static int grid_for(long long total, int block = 256, int cap = 8192) {
     return (int)g;
 }
 
-static int head_split(int B) {
-    int per = (B + 7) / 8;   // <= 8 partial slabs
-    return per < 1 ? 1 : per;
+// 64-tiles when they give >= 2 blocks per CU, else 32-tiles (bs 32 x 128^2: 512 blocks)
+static bool head_small_tiles(int B, int N) {
+    const long long t64 = (long long)ceil_div(N, 64) * ceil_div(N, 64) * B;
+    return t64 < 512;
+}
+
+template <int T>
+static void launch_head_fwd(const pu_plastic_args* a, float* hn, hipStream_t s) {
+    dim3 grid(ceil_div(a->nbf, T), ceil_div(a->nbf, T), a->batch);
+    hipLaunchKernelGGL(head_fwd_kernel<T>, grid, dim3(256), 0, s, a->x, a->hebb, a->w, a->alpha, a->y, hn, a->eta,
+                       a->nbf, a->rule);
+}
+
+template <int T>
+static void launch_head_bwd(const pu_plastic_bwd_args* a, float* ws, hipStream_t s) {
+    const int N = a->nbf, B = a->batch;
+    dim3 grid(ceil_div(N, T), ceil_div(N, T), B);
+    if (a->dx) hipLaunchKernelGGL(head_dx_kernel<T>, grid, dim3(256), 0, s, a->y, a->dy, a->hebb, a->w, a->alpha, a->dx, N);
+    if (ws) hipLaunchKernelGGL(head_dw_kernel<T>, grid, dim3(256), 0, s, a->x, a->y, a->dy, a->hebb, ws, N);
 }
 
 }  // namespace pu
@@ -344,13 +376,13 @@ extern "C" int pu_trace_update(const float* hebb, const float* x, const float* y
                                int batch, int nbf, int rule, void* stream) {
     PU_REQUIRE(hebb && x && y && eta && hebb_out && batch > 0 && nbf > 0, "pu_trace_update: bad args");
     PU_REQUIRE(rule == PU_RULE_HEBB || rule == PU_RULE_OJA, "Must select one learning rule ('hebb' or 'oja')");
-    const long long total = (long long)batch * nbf * nbf;
+    PU_REQUIRE((long long)nbf * nbf < (1ll << 31), "pu_trace_update: nbf too large");
     if (nbf % 4 == 0 && ((((uintptr_t)hebb) | ((uintptr_t)hebb_out) | ((uintptr_t)y)) & 15) == 0) {
-        hipLaunchKernelGGL(trace_kernel_v4, dim3(grid_for(total / 4, 256, 16384)), dim3(256), 0, as_stream(stream), hebb,
-                           x, y, eta, hebb_out, nbf, total / 4, rule);
+        dim3 grid(ceil_div((long long)nbf * nbf / 4, 256), batch);
+        hipLaunchKernelGGL(trace_kernel_v4, grid, dim3(256), 0, as_stream(stream), hebb, x, y, eta, hebb_out, nbf, rule);
     } else {
-        hipLaunchKernelGGL(trace_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), hebb, x, y, eta, hebb_out,
-                           nbf, total, rule);
+        dim3 grid(ceil_div((long long)nbf * nbf, 256), batch);
+        hipLaunchKernelGGL(trace_kernel, grid, dim3(256), 0, as_stream(stream), hebb, x, y, eta, hebb_out, nbf, rule);
     }
     return check_launch("pu_trace_update");
 }
@@ -358,19 +390,21 @@ extern "C" int pu_trace_update(const float* hebb, const float* x, const float* y
 extern "C" int pu_plastic_fwd(const pu_plastic_args* a, void* stream) {
     PU_REQUIRE(a && a->x && a->hebb && a->w && a->alpha && a->y && a->batch > 0 && a->nbf > 0, "pu_plastic_fwd: bad args");
     PU_REQUIRE(a->rule == PU_RULE_HEBB || a->rule == PU_RULE_OJA, "Must select one learning rule ('hebb' or 'oja')");
-    const int N = a->nbf;
-    dim3 grid(ceil_div(N, HT), ceil_div(N, HT), a->batch);
-    hipLaunchKernelGGL(head_gemm_kernel, grid, dim3(256), 0, as_stream(stream), a->x, a->hebb, a->w, a->alpha, a->y, N);
-    int st = check_launch("pu_plastic_fwd (gemm)");
-    if (st != PU_OK || !a->hebb_out) return st;
-    PU_REQUIRE(a->eta, "pu_plastic_fwd: eta missing");
-    return pu_trace_update(a->hebb, a->x, a->y, a->eta, a->hebb_out, a->batch, N, a->rule, stream);
+    PU_REQUIRE(!a->hebb_out || a->eta, "pu_plastic_fwd: eta missing");
+    // the fused update writes H' while other blocks still read H: an aliased output takes the
+    // two-launch path (GEMM, then the stand-alone update)
+    const bool fuse = a->hebb_out && a->hebb_out != a->hebb;
+    hipStream_t s = as_stream(stream);
+    float* hn = fuse ? a->hebb_out : nullptr;
+    if (head_small_tiles(a->batch, a->nbf)) launch_head_fwd<32>(a, hn, s);
+    else launch_head_fwd<64>(a, hn, s);
+    int st = check_launch("pu_plastic_fwd");
+    if (st != PU_OK || !a->hebb_out || fuse) return st;
+    return pu_trace_update(a->hebb, a->x, a->y, a->eta, a->hebb_out, a->batch, a->nbf, a->rule, stream);
 }
 
 extern "C" size_t pu_plastic_bwd_workspace_bytes(int batch, int nbf) {
-    const int per = head_split(batch);
-    const int nsplit = (batch + per - 1) / per;
-    return (size_t)nsplit * 2 * nbf * nbf * sizeof(float);
+    return (size_t)batch * 2 * nbf * nbf * sizeof(float);      // per-slot (T_b, T_b * H_b)
 }
 
 extern "C" int pu_plastic_bwd(const pu_plastic_bwd_args* a, void* workspace, size_t ws_bytes, void* stream) {
@@ -378,23 +412,19 @@ extern "C" int pu_plastic_bwd(const pu_plastic_bwd_args* a, void* workspace, siz
                "pu_plastic_bwd: bad args");
     const int N = a->nbf, B = a->batch;
     hipStream_t s = as_stream(stream);
-    if (a->dx) {
-        dim3 grid(ceil_div(N, HT), ceil_div(N, HT), B);
-        hipLaunchKernelGGL(head_dx_kernel, grid, dim3(256), 0, s, a->y, a->dy, a->hebb, a->w, a->alpha, a->dx, N);
-        int st = check_launch("pu_plastic_bwd (dx)");
-        if (st != PU_OK) return st;
-    }
+    float* ws = nullptr;
     if (a->dw || a->dalpha) {
         PU_REQUIRE(a->dw && a->dalpha, "pu_plastic_bwd: dw and dalpha go together");
         const size_t need = pu_plastic_bwd_workspace_bytes(B, N);
         if (!workspace || ws_bytes < need) return fail(PU_ERR_WORKSPACE, "pu_plastic_bwd: workspace %zu < %zu", ws_bytes, need);
-        const int per = head_split(B);
-        const int nsplit = (B + per - 1) / per;
-        dim3 grid(ceil_div(N, HT), ceil_div(N, HT), nsplit);
-        hipLaunchKernelGGL(head_dw_kernel, grid, dim3(256), 0, s, a->x, a->y, a->dy, a->hebb, (float*)workspace, N, B, per);
-        hipLaunchKernelGGL(head_dw_reduce_kernel, dim3(grid_for((long long)N * N)), dim3(256), 0, s,
-                           (const float*)workspace, nsplit, N, a->dw, a->dalpha);
+        ws = (float*)workspace;
     }
+    if (head_small_tiles(B, N)) launch_head_bwd<32>(a, ws, s);
+    else launch_head_bwd<64>(a, ws, s);
+    int st = check_launch("pu_plastic_bwd");
+    if (st != PU_OK || !ws) return st;
+    hipLaunchKernelGGL(head_dw_reduce_kernel, dim3(ceil_div((long long)N * N, 256)), dim3(256), 0, s,
+                       (const float*)ws, B, N, a->dw, a->dalpha);
     return check_launch("pu_plastic_bwd (dw)");
 }
 

@@ -8,7 +8,11 @@ not communicated.
 
 Gradients land in ONE flat fp32 buffer: the trunk/head backward kernels write straight into views
 of it (autograd adopts those views as ``param.grad``), so the all-reduce needs no pack/unpack
-copies.  The all-reduce is split into a few large buckets issued in reverse layer order.
+copies.  The buffer is laid out in the order the backward produces gradients (head first, then
+the trunk from its output layer down to the stem), and ``BucketReducer`` issues an asynchronous
+all-reduce for each contiguous bucket the moment its last gradient kernel has been enqueued, so
+RCCL runs on its own stream under the remaining backward kernels (overlap); ``finish`` makes the
+compute stream wait for the last bucket before Adam.
 """
 import os
 
@@ -43,25 +47,36 @@ def broadcast_params(module, src=0):
 
 
 class GradBuffer:
-    """Flat gradient storage for ``params`` (in order); ``views[i]`` has ``params[i]``'s shape."""
+    """Flat gradient storage for ``params`` (in order); ``views[i]`` has ``params[i]``'s shape.
+    Every view starts on a 256-byte boundary (``ALIGN`` floats), so the vectorised kernels that
+    write and read gradients (wgrad epilogues, Adam) keep their 16-byte accesses whatever the
+    parameter sizes are (the outconv bias has 1 element); the padding is zero and never read."""
+
+    ALIGN = 64
 
     def __init__(self, params, device):
         self.params = list(params)
-        self.numel = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
-        self.views = []
+        self.reducer = None      # BucketReducer: notified by the backward as gradients complete
         self.offsets = {}
         off = 0
         for p in self.params:
-            self.views.append(self.flat[off:off + p.numel()].view_as(p))
             self.offsets[id(p)] = (off, p.numel())
-            off += p.numel()
+            off += (p.numel() + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.numel = off
+        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.views = [self.flat[o:o + n].view_as(p) for p, (o, n) in
+                      ((p, self.offsets[id(p)]) for p in self.params)]
 
     def view_for(self, p):
         o = self.offsets.get(id(p))
         if o is None:
             return None
         return self.flat[o[0]:o[0] + o[1]].view_as(p)
+
+    def ready(self, *params):
+        """Called by the backward right after enqueuing the kernels that write ``params``' grads."""
+        if self.reducer is not None:
+            self.reducer.ready(params)
 
     def owns_grads(self):
         base = self.flat.data_ptr()
@@ -107,3 +122,85 @@ def allreduce_grads(params, gradbuf=None, group=None, bucket_mb=32):
     for g in grads:
         g.copy_(flat[off:off + g.numel()].view_as(g))
         off += g.numel()
+
+
+class BucketReducer:
+    """Overlapped gradient averaging over a GradBuffer.
+
+    The flat buffer is cut into contiguous buckets of about ``bucket_mb`` (never splitting a
+    parameter).  ``begin()`` arms it before backward; every ``ready(params)`` call counts those
+    parameters off their bucket, and a bucket whose last parameter arrives is all-reduced at once
+    with ``async_op=True`` (RCCL runs on its own stream, ordered after the kernels already enqueued
+    on the compute stream).  Every rank runs the same backward, so buckets are issued in the same
+    order on all ranks.  ``finish()`` issues whatever is left (parameters that never reported, in
+    buffer order), then waits: on RCCL ``wait`` only orders the current stream after the
+    collective, so the host does not block."""
+
+    def __init__(self, gradbuf, bucket_mb=16, group=None):
+        self.gb = gradbuf
+        self.group = group
+        cap = max(1, int(bucket_mb * (1 << 20)) // 4)
+        self.buckets = []        # [start, end, {param ids}]
+        self.bucket_of = {}
+        start, ids = 0, set()
+        off = 0
+        for p in gradbuf.params:
+            off = gradbuf.offsets[id(p)][0]
+            n = gradbuf.offsets[id(p)][1]
+            if ids and off + n - start > cap:
+                self.buckets.append((start, off, ids))
+                start, ids = off, set()
+            ids.add(id(p))
+            self.bucket_of[id(p)] = len(self.buckets)
+            off += n
+        if ids:
+            self.buckets.append((start, off, ids))
+        self.works = []
+        self.pending = None
+        self.issued = None
+        self.active = False
+
+    def begin(self):
+        self.pending = [set(b[2]) for b in self.buckets]
+        self.issued = [False] * len(self.buckets)
+        self.works = []
+        self.active = dist.is_initialized() and dist.get_world_size(self.group) > 1
+        self.gb.reducer = self if self.active else None
+
+    def _issue(self, k):
+        s, e, _ = self.buckets[k]
+        t = self.gb.flat[s:e]
+        gloo = dist.get_backend(self.group) == "gloo"
+        op = dist.ReduceOp.SUM if gloo else dist.ReduceOp.AVG
+        self.works.append((dist.all_reduce(t, op=op, group=self.group, async_op=True), t, gloo))
+        self.issued[k] = True
+
+    def ready(self, params):
+        if not self.active:
+            return
+        for p in params:
+            k = self.bucket_of.get(id(p))
+            if k is None or self.issued[k]:
+                continue
+            self.pending[k].discard(id(p))
+            if not self.pending[k]:
+                self._issue(k)
+
+    def finish(self):
+        """Issue the remaining buckets, then order the current stream after every all-reduce.
+        Returns the number of buckets that were issued during backward (overlapped)."""
+        if not self.active:
+            return 0
+        early = sum(self.issued)
+        for k in range(len(self.buckets)):
+            if not self.issued[k]:
+                self._issue(k)
+        world = dist.get_world_size(self.group)
+        for w, t, gloo in self.works:
+            w.wait()
+            if gloo:
+                t.div_(world)
+        self.works = []
+        self.active = False
+        self.gb.reducer = None
+        return early

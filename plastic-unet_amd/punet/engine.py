@@ -1,7 +1,7 @@
 """Batched training step of the plastic U-Net (the hot loop of src/train.py:91-112, batched).
 
     trainer = Trainer(net, lr=3e-4, steplr=1e5)     # FusedAdam + StepLR(gamma .666), per step
-    loss, hebb = trainer.step(x, t, hebb)           # fwd -> BCE -> bwd -> [RCCL all-reduce] -> Adam
+    loss, hebb = trainer.step(x, t, hebb)           # fwd -> BCE -> bwd (+ overlapped RCCL all-reduce) -> Adam
 
 Batched semantics: slot b of step s carries its trace to slot b of step
 s+1; loss = mean BCE over all slots' pixels (so each slot contributes the reference's per-sample
@@ -18,18 +18,27 @@ from .optim import FusedAdam
 
 class Trainer:
     def __init__(self, net, lr=3e-4, steplr=1e5, gamma=0.666, betas=(0.9, 0.999), eps=1e-8,
-                 flat_grads=True, bucket_mb=32):
+                 flat_grads=True, bucket_mb=16, overlap=True):
         self.net = net
         self.params = list(net.parameters())
         self.opt = FusedAdam(net.parameters(), lr=lr, betas=betas, eps=eps)
         self.sched = torch.optim.lr_scheduler.StepLR(self.opt, gamma=gamma, step_size=int(steplr))
         self.bucket_mb = bucket_mb
         self.gradbuf = None
-        if flat_grads and hasattr(net, "_trunk_plan"):
-            trainable = [p for p in self.params if p is not net.eta]
-            self.gradbuf = dp.GradBuffer(trainable, next(net.parameters()).device)
-            net._trunk_plan().gradbuf = self.gradbuf
+        self.reducer = None
         self.distributed = dist.is_initialized() and dist.get_world_size() > 1
+        if flat_grads and hasattr(net, "_trunk_plan"):
+            # flat buffer in gradient-completion order: head (w, alpha), then the trunk's backward order
+            trunk = net._trunk_plan()
+            order = [net.w, net.alpha] + trunk.backward_order()
+            seen = set(id(p) for p in order)
+            order += [p for p in self.params if id(p) not in seen]
+            trainable = [p for p in order if p is not net.eta]
+            self.gradbuf = dp.GradBuffer(trainable, next(net.parameters()).device)
+            trunk.gradbuf = self.gradbuf
+            if self.distributed and overlap:
+                self.reducer = dp.BucketReducer(self.gradbuf, bucket_mb=bucket_mb)
+        self.overlapped_buckets = 0
 
     def step(self, x, t, hebb):
         """One optimisation step on the local batch.  Returns (loss tensor, new hebb), both
@@ -38,8 +47,14 @@ class Trainer:
             p.grad = None
         y, hn = self.net(x, hebb.detach())
         loss = bce_loss(y, t)
+        if self.reducer is not None:
+            self.reducer.begin()          # buckets all-reduce (async) as the backward completes them
         loss.backward()
-        if self.distributed:
+        if self.reducer is not None:
+            self.overlapped_buckets = self.reducer.finish()
+            if not self.gradbuf.owns_grads():       # grads did not land in the buffer: reduce them
+                dp.allreduce_grads(self.params, None)
+        elif self.distributed:
             dp.allreduce_grads(self.params, self.gradbuf, bucket_mb=self.bucket_mb)
         self.opt.step()
         self.sched.step()

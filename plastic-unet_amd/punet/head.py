@@ -48,6 +48,8 @@ class PlasticHeadFunction(torch.autograd.Function):
             if wp.grad is None and ap.grad is None:
                 out = (gb.view_for(wp), gb.view_for(ap))
         dx, dw, da = K.plastic_bwd(X, H, w, alpha, y, dy.contiguous(), need_dx=need_dx, need_dw=need_dw, out=out)
+        if out is not None:
+            ctx.sink[0].ready(ctx.sink[1], ctx.sink[2])
         return (dx, None, dw if ctx.needs_input_grad[2] else None, da if ctx.needs_input_grad[3] else None,
                 None, None, None, None)
 

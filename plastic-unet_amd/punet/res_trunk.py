@@ -170,6 +170,16 @@ class ResTrunk:
                 out += [cm.conv.weight, cm.conv.bias]
         return out
 
+    def backward_order(self):
+        """Parameters in the order backward() completes their gradients (outc first, conv1 last)."""
+        return list(reversed(self.params))
+
+    def _ready(self, i, n=2):
+        """params[i:i+n]'s gradient kernels are enqueued: let an armed BucketReducer know."""
+        gb = self.gradbuf
+        if gb is not None and gb.reducer is not None:
+            gb.ready(*self.params[i:i + n])
+
     def grad_sinks(self):
         gb = self.gradbuf
         if gb is None or any(p.grad is not None for p in self.params):
@@ -235,14 +245,19 @@ class ResTrunk:
         x0, x1, r1, a1, r2, a2, y = st
         dbg = self.debug
         grads[i + 8], grads[i + 9] = conv3x3_wgrad(g, a2, out=out(i + 8))
+        self._ready(i + 8)
         g_a2, _ = conv3x3_dgrad(g, P[i + 8], pk, mask0=a2)
         grads[i + 6], grads[i + 7] = conv3x3_wgrad(g_a2, r2, out=out(i + 6))
+        self._ready(i + 6)
         g_o1, _ = conv3x3_dgrad(g_a2, P[i + 6], pk, mask0=r2, resid=g)
         grads[i + 4], grads[i + 5] = conv3x3_wgrad(g_o1, a1, out=out(i + 4))
+        self._ready(i + 4)
         g_a1, _ = conv3x3_dgrad(g_o1, P[i + 4], pk, mask0=a1)
         grads[i + 2], grads[i + 3] = conv3x3_wgrad(g_a1, r1, out=out(i + 2))
+        self._ready(i + 2)
         g_z0, _ = conv3x3_dgrad(g_a1, P[i + 2], pk, mask0=r1, resid=g_o1)
         grads[i], grads[i + 1] = conv3x3_wgrad(g_z0, x0, x1, out=out(i))
+        self._ready(i)
         if dbg is not None:
             dbg[i] = (g, g_a2, g_o1, g_a1, g_z0)
         if not need_dx:
@@ -262,6 +277,7 @@ class ResTrunk:
                                     out=None if oo is None else (oo[0].view(-1), oo[1]))
         grads[o] = dwo.view_as(P[o])
         grads[o + 1] = dbo
+        self._ready(o)
         gskip = [None] * 4
         for j in range(3, -1, -1):                       # uconv1 .. uconv4
             name = self.UP[j]
@@ -277,6 +293,7 @@ class ResTrunk:
             i = self.slots[name + ".up"]
             x_in = s[name + ".in"]
             grads[i], grads[i + 1] = convT3x3_wgrad(x_in, g_u, out=out(i))
+            self._ready(i)
             g = convT3x3_dgrad(g_u, P[i], self.packs, x_in.shape[1:3], mask=x_in)
         g_p, _ = self._stack_bwd(P, self.slots["mid"], s["mid"], g, grads, out)
         for k in range(3, -1, -1):                       # conv4 .. conv1

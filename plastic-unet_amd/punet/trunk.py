@@ -189,6 +189,17 @@ class UNetpTrunk:
         self.gradbuf = None      # punet.dp.GradBuffer: backward writes grads into its views
         self.debug = None        # dict: when set, backward stores each layer's dZ (tests/diagnostics)
 
+    def backward_order(self):
+        """Parameters in the order backward() completes their gradients (outc first, stem last)."""
+        core = self.params[:-2] if self.coord is not None else self.params
+        return list(reversed(core)) + (self.params[-2:] if self.coord is not None else [])
+
+    def _ready(self, i, n=2):
+        """params[i:i+n]'s gradient kernels are enqueued: let an armed BucketReducer know."""
+        gb = self.gradbuf
+        if gb is not None and gb.reducer is not None:
+            gb.ready(*self.params[i:i + n])
+
     def grad_sinks(self):
         """Views of the flat gradient buffer to write into, or None.  Only used when every
         parameter's .grad is None (autograd then adopts the views; if a .grad already existed it
@@ -260,6 +271,7 @@ class UNetpTrunk:
                                     out=None if o is None else (o[0].view(-1), o[1]))
         grads[outc] = dwo.view_as(P[outc])
         grads[outc + 1] = dbo
+        self._ready(outc)
 
         gskip = [None] * (D - 1)
         for j in range(D - 1, 0, -1):
@@ -272,13 +284,16 @@ class UNetpTrunk:
                 self.debug["up%d.c1" % j] = g
             # conv1 of up_j: y_j = relu(conv(t));  g = dZ
             grads[base + 4], grads[base + 5] = conv3x3_wgrad(g, t, out=out(base + 4))
+            self._ready(base + 4)
             dt, _ = conv3x3_dgrad(g, P[base + 4], pk, mask0=t)
             # conv0 over [skip | u]  (up_first: [u | skip])
             if self.up_first:
                 grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, u, skip, out=out(base + 2))
+                self._ready(base + 2)
                 du, dskip = conv3x3_dgrad(dt, P[base + 2], pk, split=u.shape[3], mask1=skip)
             else:
                 grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, skip, u, out=out(base + 2))
+                self._ready(base + 2)
                 dskip, du = conv3x3_dgrad(dt, P[base + 2], pk, split=skip.shape[3], mask0=skip)
             if self.debug is not None:
                 self.debug["up%d.c0" % j] = dt
@@ -286,6 +301,7 @@ class UNetpTrunk:
             gskip[D - 1 - j] = dskip
             # ConvT
             grads[base], grads[base + 1] = convT2x2_wgrad(y_prev, du, out=out(base))
+            self._ready(base)
             g = convT2x2_dgrad(du, P[base], pk, mask=y_prev)
 
         for i in range(D - 1, 0, -1):
@@ -295,8 +311,10 @@ class UNetpTrunk:
             if self.debug is not None:
                 self.debug["down%d.c1" % i] = g
             grads[base + 2], grads[base + 3] = conv3x3_wgrad(g, t, out=out(base + 2))
+            self._ready(base + 2)
             dt, _ = conv3x3_dgrad(g, P[base + 2], pk, mask0=t)
             grads[base], grads[base + 1] = conv3x3_wgrad(dt, p, out=out(base))
+            self._ready(base)
             if self.debug is not None:
                 self.debug["down%d.c0" % i] = dt
             dp, _ = conv3x3_dgrad(dt, P[base], pk)
@@ -306,11 +324,13 @@ class UNetpTrunk:
         if self.debug is not None:
             self.debug["inc.c1"] = g
         grads[2], grads[3] = conv3x3_wgrad(g, t, out=out(2))
+        self._ready(2)
         dt, _ = conv3x3_dgrad(g, P[2], pk, mask0=t)
         x0 = s["stem"] if self.coord is not None else s["x"]
         if dt.dtype != x0.dtype:       # bf16 trunk: the fp32 stem's weight gradient
             dt = K.to_f32(dt)
         grads[0], grads[1] = conv3x3_wgrad(dt, x0, out=out(0))
+        self._ready(0)
         if self.debug is not None:
             self.debug["inc.c0"] = dt
         if self.coord is not None:     # stem 1x1 conv: dgrad of inc.c0 (masked by the stem ReLU) + wgrad
@@ -323,6 +343,7 @@ class UNetpTrunk:
             K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, rows=dstem, n=P[cs].shape[0],
                     src0=s["x"], c0=ca, bias_mode=1, dweight=dw, dbias=db)
             grads[cs], grads[cs + 1] = dw, db
+            self._ready(cs)
         return grads
 
 

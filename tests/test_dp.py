@@ -81,3 +81,47 @@ def test_dp_two_ranks_match_single_process(tmp_path, use_gradbuf):
             torch.testing.assert_close(r["grads"][n], p.grad, rtol=1e-5, atol=1e-9)
     for r in res:                                          # traces are per rank, never synchronised
         torch.testing.assert_close(r["hebb"], hn[r["lo"]:r["hi"]].detach(), rtol=1e-6, atol=1e-8)
+
+
+def _reducer_worker(rank, world, port, out_dir):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from punet import dp
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    shapes = [(300,), (17, 9), (1000,), (5,), (64, 3, 3), (2,), (4000,)]
+    params = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+    gb = dp.GradBuffer(params, "cpu")
+    red = dp.BucketReducer(gb, bucket_mb=1000 * 4 / (1 << 20))     # ~1000 floats per bucket
+    assert len(red.buckets) >= 3
+    for step in range(2):
+        for i, v in enumerate(gb.views):
+            v.copy_(torch.arange(v.numel(), dtype=torch.float32).view_as(v) * (rank + 1) + 100 * i + step)
+        red.begin()
+        # completion order as a backward would report it, one parameter never reported
+        for i in (6, 5, 4, 3, 1, 0):     # param 2 (a bucket of its own) never reports
+            gb.ready(params[i])
+        early = red.finish()
+        assert early >= 1                    # at least one bucket went out during "backward"
+        assert gb.reducer is None
+        torch.save([v.clone() for v in gb.views], os.path.join(out_dir, "red%d_%d.pt" % (rank, step)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bucket_reducer_two_ranks(tmp_path):
+    """Overlapped bucketed averaging (punet.dp.BucketReducer): every bucket is averaged exactly
+    once, including buckets whose parameters never reported ready, and the reducer disarms."""
+    world = 2
+    mp.spawn(_reducer_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    shapes = [(300,), (17, 9), (1000,), (5,), (64, 3, 3), (2,), (4000,)]
+    for step in range(2):
+        got = [torch.load(os.path.join(tmp_path, "red%d_%d.pt" % (r, step)), weights_only=True) for r in range(world)]
+        for i, s in enumerate(shapes):
+            n = int(torch.tensor(s).prod())
+            base = torch.arange(n, dtype=torch.float32).view(s)
+            want = sum(base * (r + 1) + 100 * i + step for r in range(world)) / world
+            for r in range(world):
+                torch.testing.assert_close(got[r][i], want)

@@ -257,3 +257,27 @@ def test_fused_adam_matches_torch_adam():
         o1.step(); o2.step(); s1.step(); s2.step()
     for a, b in zip(ref, dev):
         assert_close(b, a, rtol=1e-6, atol_rel=1e-6)
+
+
+@pytest.mark.parametrize("B,N", [(32, 128), (128, 128), (3, 50), (2, 200), (1, 512)])
+@pytest.mark.parametrize("rule", [0, 1])
+def test_fused_head_trace_equals_two_launch_path(B, N, rule):
+    """pu_plastic_fwd fuses the trace update into the GEMM (every block recomputes row 0 of its
+    column tile).  It must equal, bit for bit, the GEMM followed by the stand-alone update on its
+    own Y (the in-place call takes that path), for both tile sizes (32: small grids, 64) and
+    ragged N."""
+    g = torch.Generator().manual_seed(B * 1000 + N)
+    X = rnd(B, N, N, g=g, scale=2.0).to(DEV)
+    H = rnd(B, N, N, g=g, scale=0.2).to(DEV)
+    w = rnd(N, N, g=g, scale=0.05).to(DEV)
+    al = (torch.rand(N, N, generator=g) * 0.05).to(DEV)
+    eta = torch.tensor([0.0173], device=DEV)
+    Y, Hn = K.plastic_fwd(X, H, w, al, eta, rule, True)
+    Y2, none = K.plastic_fwd(X, H, w, al, eta, rule, False)
+    assert none is None
+    assert torch.equal(Y, Y2)
+    Hn2 = K.trace_update(H, X, Y2, eta, rule)
+    assert torch.equal(Hn, Hn2)
+    Yr, Hr = oracle.plastic_head(X.cpu(), H.cpu(), w.cpu(), al.cpu(), eta.cpu(), "hebb" if rule == 0 else "oja")
+    assert_close(Y, Yr)
+    assert_close(Hn, Hr)
