@@ -104,13 +104,22 @@ typedef struct {
     void* workspace; size_t ws_bytes;
     const float* resid;
     int shuf_h, shuf_w, shuf_off;
+    /* optional: `weight` split into bf16 planes by pu_split_weight6.  When set, the MFMA path
+     * computes each fp32 product as 6 exact bf16 products (hi/mid/lo terms, fp32 accumulation;
+     * dropped terms < 2^-23 relative) on v_mfma_f32_32x32x16_bf16 - 2.7x the fp32-MFMA rate.
+     * Layers that take another kernel (small-channel direct, odd channel counts) use `weight`. */
+    const void* weight6;
 } pu_conv_args;
 
 int pu_conv_igemm(const pu_conv_args* a, void* stream);
+/* packed fp32 weight [n][k_pad] -> bf16 planes [k_pad/16][6][n][8] (q = plane*2 + (k%16)/8; plane
+ * 0/1/2 = hi/mid/lo, w == hi + mid + lo exactly); out holds n*k_pad*3 bf16 (6 bytes per weight) */
+int pu_split_weight6(const float* packed, void* out, int n, int k_pad, void* stream);
 /* split-K scratch pu_conv_igemm would use for these arguments (0: no split planned) */
 size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a);
 /* the kernel instantiation pu_conv_igemm would launch: block tile bm x bn, A-loader mode
- * (0 = 16-channel chunks, 1 = float4, 2 = scalar) and K splits (1 = none; counts a->workspace);
+ * (0 = 16-channel chunks, 1 = float4, 2 = scalar, 3 = small-channel direct, 4 = 16-channel
+ * chunks on the 6-product bf16 kernel) and K splits (1 = none; counts a->workspace);
  * for profiling/roofline attribution */
 int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* mode, int* ksplit);
 
@@ -137,6 +146,9 @@ typedef struct {
     float* dweight;
     float* dbias;
     int accumulate;
+    /* fp32 GEMM arithmetic: 0 = v_mfma_f32_32x32x2_f32; 1 = each product as 6 exact bf16 products
+     * (hi/mid/lo split of both operands, fp32 accumulation) on v_mfma_f32_32x32x16_bf16 */
+    int math;
 } pu_wgrad_args;
 
 size_t pu_wgrad_workspace_bytes(const pu_wgrad_args* a);

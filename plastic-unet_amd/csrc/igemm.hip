@@ -562,6 +562,258 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
     }
 }
 
+// ------------------------------------------------------------- fp32 GEMM as 6 bf16 MFMA products
+// gfx950 has one fp32 matrix op, v_mfma_f32_32x32x2_f32 (64 cycles per 32x32x2), 1/16 of the bf16
+// rate.  An fp32 value splits EXACTLY into three bf16 terms x = x_hi + x_mid + x_lo (round to
+// nearest at each step: |x_mid| <= 2^-8 |x|, |x_lo| <= 2^-16 |x|, and the last residual has at
+// most 8 significant bits), so
+//   x*y = x_hi y_hi + (x_hi y_mid + x_mid y_hi) + (x_hi y_lo + x_lo y_hi + x_mid y_mid) + O(2^-24 xy)
+// takes 6 v_mfma_f32_32x32x16_bf16 (exact bf16 products, fp32 accumulation) per 16 k: 192
+// cycles against the 512 of eight f32 MFMAs - the fp32 path on the bf16 pipe, with the error of
+// an fp32 product (the dropped terms are below 2^-23 relative).
+// Weights come pre-split (pu_split_weight6: [k/16][q = plane*2 + half][n][8 bf16]); pixel rows
+// are staged as fp32 exactly like igemm_dma_kernel and split after the LDS read (VALU work that
+// co-issues with the MFMAs).  Same loader, ring, swizzle, epilogue and split-K as the fp32 kernel.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf16x8_t& h, bf16x8_t& m, bf16x8_t& l) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float x = e < 4 ? lo4[e] : hi4[e - 4];
+        const __bf16 a = (__bf16)x;
+        const float r = x - (float)a;
+        const __bf16 b = (__bf16)r;
+        const float q = r - (float)b;
+        h[e] = a;
+        m[e] = b;
+        l[e] = (__bf16)q;
+    }
+}
+
+#ifndef PU_X6_KSUB
+#define PU_X6_KSUB 1     // 16-k sub-stages per LDS ring slot / barrier (exploration knob)
+#endif
+#ifndef PU_X6_SCHED
+#define PU_X6_SCHED 1    // 0: next-stage loads issued before the MFMAs; 1: after the first sub-tile's
+#endif
+#ifndef PU_X6_NBUF
+#define PU_X6_NBUF 3
+#endif
+
+template <int BM, int BN, int WM, int WN, int NBUF, int KSUB>
+__global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
+    constexpr int FM = BM / WM / 32;
+    constexpr int FN = BN / WN / 32;
+    constexpr int A_LD = BM / 64;             // pixel rows: glds per wave per sub-stage (16 rows x 64 B)
+    constexpr int W_TOT = 6 * BN / 64;        // weight planes: glds per block per sub-stage (64 x 16 B)
+    constexpr int W_LD = (W_TOT + 3) / 4;     // per wave (surplus ones load the zero page into a sink)
+    constexpr bool SINK = (W_TOT % 4) != 0;
+    constexpr int G = (A_LD + W_LD) * KSUB;   // loads per wave per ring slot
+    constexpr int A_FL = BM * 16;             // floats of one sub-stage's pixel image
+    constexpr int W_FL = BN * 6 * 4;          // float-sized slots of one sub-stage's weight planes
+    constexpr int SUB = A_FL + W_FL;
+    constexpr int STAGE = KSUB * SUB;
+    static_assert(WM * WN == 4, "4 waves");
+
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE + (SINK ? 256 : 0)];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int lr = lane & 31, lh = lane >> 5;
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kz = tile / (gridDim.x / p.ksplit);
+    tile -= kz * (gridDim.x / p.ksplit);
+    const int mb = tile / p.gn;
+    const int m_blk = mb * BM;
+    const int n_blk = (tile - mb * p.gn) * BN;
+
+    const int lq = lane >> 2;
+    const int kc = (lane & 3) ^ ((lane >> 4) & 3);
+    long long rb0[A_LD], rb1[A_LD];
+    unsigned tmask[A_LD];
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) {
+        const int m = m_blk + wave * (BM / 4) + 16 * j + lq;
+        rb0[j] = 0; rb1[j] = 0; tmask[j] = 0;
+        if (m < p.M) {
+            const int t = fdiv(m, p.dWo);
+            const int wo = m - t * p.Wo;
+            const int b = fdiv(t, p.dHo);
+            const int ho = t - b * p.Ho;
+            const int hb = ho * p.stride - p.pad, wb = wo * p.stride - p.pad;
+            const long long pix0 = (long long)b * p.Hi * p.Wi + (long long)hb * p.Wi + wb;
+            rb0[j] = pix0 * p.c0 + kc * 4;
+            rb1[j] = pix0 * p.c1 + kc * 4;
+            unsigned msk = 0;
+            for (int r = 0; r < p.kh; ++r)
+                for (int q = 0; q < p.kw; ++q)
+                    if ((unsigned)(hb + r) < (unsigned)p.Hi && (unsigned)(wb + q) < (unsigned)p.Wi)
+                        msk |= 1u << (r * p.kw + q);
+            tmask[j] = msk;
+        }
+    }
+    // weight-plane loads: block instruction I = wave + 4j covers entries [64 I, 64 I + 64) of the
+    // sub-stage's [q][BN] image (one plane-half q, contiguous rows -> one coalesced 1 KB read)
+    const __bf16* w6 = reinterpret_cast<const __bf16*>(p.wt);
+    const __bf16* wrow[W_LD];
+#pragma unroll
+    for (int j = 0; j < W_LD; ++j) {
+        const int I = wave + 4 * j;
+        const int e = I * 64 + lane;
+        const int q = e / BN, row = e - q * BN;
+        const int n = n_blk + row;
+        wrow[j] = (I < W_TOT && n < p.N) ? w6 + ((long long)q * p.N + n) * 8 : nullptr;
+    }
+    const long long w_stage = 6LL * p.N * 8;   // bf16 elements per 16-k sub-stage
+
+    const int t0 = kz * p.t_per;
+    const int T = min(p.k_pad / IG_BK - t0, p.t_per);     // 16-k sub-stages of this split
+    const int TS = (T + KSUB - 1) / KSUB;                  // ring slots
+    auto issue_sub = [&](int tl, float* a_slot) {
+        const bool live = tl < T;
+        const int t = t0 + (live ? tl : 0);
+        const int k0 = t * IG_BK;
+        const bool two = p.cgroup == 32;
+        const int tg = two ? (t >> 1) : t;
+        const int g = fdiv(tg, p.dTaps);
+        const int tap_n = fdiv(k0, p.dC);
+        const int tap = p.cgroup ? tg - g * p.taps : tap_n;
+        const int c = p.cgroup ? g * p.cgroup + (two ? (t & 1) * 16 : 0) : k0 - tap_n * p.C;
+        const int r = fdiv(tap, p.dKw);
+        const int s = tap - r * p.kw;
+        const bool first = c < p.c0;
+        const float* src = first ? p.src0 : p.src1;
+        const int cs = first ? p.c0 : p.c1;
+        const long long off = (long long)(r * p.Wi + s) * cs + (first ? c : c - p.c0);
+        const unsigned bit = (live && k0 < p.K) ? (1u << tap) : 0u;
+        const long long wo = (long long)t * w_stage;
+        float* w_slot = a_slot + A_FL;
+#pragma unroll
+        for (int j = 0; j < A_LD; ++j) {
+            const float* g = (tmask[j] & bit) ? src + (first ? rb0[j] : rb1[j]) + off : g_zero16;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(a_slot + (wave * (BM / 4) + 16 * j) * 16),
+                                             16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < W_LD; ++j) {
+            const int I = wave + 4 * j;
+            const void* g = (live && wrow[j]) ? (const void*)(wrow[j] + wo) : (const void*)g_zero16;
+            float* dst = (!SINK || I < W_TOT) ? w_slot + I * 256 : lds + NBUF * STAGE;   // 64 lanes x 16 B
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)dst, 16, 0, 0);
+        }
+    };
+    auto issue = [&](int ts, int slot) {
+#pragma unroll
+        for (int u = 0; u < KSUB; ++u) issue_sub(ts * KSUB + u, lds + slot * STAGE + u * SUB);
+    };
+
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int a_row0 = wm * (BM / WM) + lr;
+    const int b_row0 = wn * (BN / WN) + lr;
+    const int swz = (lr >> 2) & 3;
+    const int pos0 = ((2 * lh) ^ swz) * 4, pos1 = ((2 * lh + 1) ^ swz) * 4;
+
+#pragma unroll
+    for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(s0, s0);
+
+    for (int ts = 0; ts < TS; ++ts) {
+        // ring slot ts landed when only the NBUF-2 younger slots' loads are pending
+        if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        else if (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+        __builtin_amdgcn_s_barrier();
+        const float* slot = lds + (ts % NBUF) * STAGE;
+#pragma unroll
+        for (int u = 0; u < KSUB; ++u) {
+            const float* a = slot + u * SUB;
+            const float* wp = a + A_FL;
+            f32x4 xa[FM], xb[FM];
+            bf16x8_t fw[3][FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                xa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos0);
+                xb[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos1);
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    fw[pl][j] = *reinterpret_cast<const bf16x8_t*>(wp + ((pl * 2 + lh) * BN + b_row0 + j * 32) * 4);
+            if (PU_X6_SCHED == 0 && u == 0) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                bf16x8_t xh, xm, xl;
+                split3_bf16(xa[i], xb[i], xh, xm, xl);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    f32x16 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xm, c, 0, 0, 0);   // small terms first
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[2][j], xh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xl, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xm, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xh, c, 0, 0, 0);
+                    acc[i][j] = c;
+                }
+                if (PU_X6_SCHED == 1 && u == 0 && i == 0) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (p.ksplit == 1) {
+        epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
+        return;
+    }
+    float* part = p.part + (long long)kz * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                if (n >= p.N) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                *reinterpret_cast<f32x4*>(part + (long long)m * p.N + n) = v;
+            }
+    }
+}
+
+// packed fp32 weight [n][k_pad] -> [k_pad/16][q][n][8] bf16 planes, q = plane*2 + (k%16)/8,
+// plane 0/1/2 = hi/mid/lo of the round-to-nearest split (exact: hi + mid + lo == w)
+__global__ void split_weight6_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int n, int k_pad) {
+#pragma clang fp contract(off)
+    const long long total = (long long)n * k_pad;
+    for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
+        const int row = (int)(idx / k_pad);
+        const int k = (int)(idx - (long long)row * k_pad);
+        const float x = w[idx];
+        const __bf16 a = (__bf16)x;
+        const float r = x - (float)a;
+        const __bf16 b = (__bf16)r;
+        const __bf16 c = (__bf16)(r - (float)b);
+        const int t = k >> 4, half = (k >> 3) & 1, e = k & 7;
+        const __bf16 v[3] = {a, b, c};
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            out[(((long long)t * 6 + pl * 2 + half) * n + row) * 8 + e] = v[pl];
+    }
+}
+
 // split-K second pass: sum the partial tiles in split order (deterministic) + the fused epilogue
 __global__ __launch_bounds__(256) void igemm_splitk_epilogue_kernel(const IgemmParams p) {
     const int nq = p.N >> 2;
@@ -854,7 +1106,16 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     }
     p.part = (float*)a->workspace;
     const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
-    if (mode == LOAD_CHUNK16 && !PU_NO_DMA) {
+    if (a->weight6 && mode == LOAD_CHUNK16 && !PU_NO_DMA) {
+        p.wt = reinterpret_cast<const float*>(a->weight6);
+        PU_REQUIRE(((uintptr_t)a->weight6 & 15) == 0, "pu_conv_igemm: weight6 must be 16-byte aligned");
+#define PU_X6(BM_, BN_, WM_, WN_) hipLaunchKernelGGL((igemm_x6_kernel<BM_, BN_, WM_, WN_, PU_X6_NBUF, PU_X6_KSUB>), grid, dim3(256), 0, s, p)
+        if (bm == 256) PU_X6(256, 64, 4, 1);
+        else if (bm == 128 && bn == 128) PU_X6(128, 128, 2, 2);
+        else if (bm == 128) PU_X6(128, 64, 2, 2);
+        else PU_X6(64, 64, 2, 2);
+#undef PU_X6
+    } else if (mode == LOAD_CHUNK16 && !PU_NO_DMA) {
         if (bm == 256) hipLaunchKernelGGL((igemm_dma_kernel<256, 64, 4, 1, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
         else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 128, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
         else if (bm == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 64, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
@@ -868,6 +1129,16 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         hipLaunchKernelGGL(igemm_splitk_epilogue_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, p);
     }
     return check_launch("pu_conv_igemm");
+}
+
+extern "C" int pu_split_weight6(const float* packed, void* out, int n, int k_pad, void* stream) {
+    PU_REQUIRE(packed && out && n > 0 && k_pad > 0 && k_pad % IG_BK == 0, "pu_split_weight6: bad args");
+    const long long total = (long long)n * k_pad;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(split_weight6_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), packed,
+                       (__bf16*)out, n, k_pad);
+    return check_launch("pu_split_weight6");
 }
 
 extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
@@ -885,6 +1156,7 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
     const long long M = (long long)a->batch * a->out_h * a->out_w;
     choose_tile(M, a->n, bm, bn);
     *mode = choose_mode(a->c0, a->c1);
+    if (a->weight6 && *mode == LOAD_CHUNK16 && !PU_NO_DMA && !small_conv_ok(a)) *mode = 4;   // 6-product bf16
     if (small_conv_ok(a)) {          // reported as mode 3 ("direct"), tile SC_TH x SC_TW pixels
         *bm = SC_TH * SC_TW;
         *bn = a->n;

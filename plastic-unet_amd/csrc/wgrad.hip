@@ -239,7 +239,26 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 __device__ __attribute__((aligned(16))) float g_wg_zero16[4] = {0.f, 0.f, 0.f, 0.f};
 
-template <int BN, int BK, int WN, int WK, int NBUF>
+typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
+
+// 8 fp32 values -> their exact 3-term bf16 split (see igemm.hip, igemm_x6_kernel)
+__device__ __forceinline__ void wg_split3(const float (&x)[8], wg_bf16x8& h, wg_bf16x8& m, wg_bf16x8& l) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const __bf16 a = (__bf16)x[e];
+        const float r = x[e] - (float)a;
+        const __bf16 b = (__bf16)r;
+        h[e] = a;
+        m[e] = b;
+        l[e] = (__bf16)(r - (float)b);
+    }
+}
+
+// X6: the 16 staged pixel rows are one k-step of v_mfma_f32_32x32x16_bf16 and each fp32 product
+// is 6 exact bf16 products (hi/mid/lo split, fp32 accumulation) - 6 x 32 cycles against the
+// 8 x 64 of v_mfma_f32_32x32x2_f32; lane (i, h) reads rows 8h..8h+7 of its column.
+template <int BN, int BK, int WN, int WK, int NBUF, bool X6>
 __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
     constexpr int FN = BN / WN / 32;
     constexpr int FK = BK / WK / 32;
@@ -357,6 +376,37 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
         __builtin_amdgcn_s_barrier();
         const float* ps = lds + (t % NBUF) * STAGE;
         const float* qs = ps + WG_BM * BN;
+        if constexpr (X6) {
+            float xa[FN][8], xb[FK][8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int row = 8 * lh + e;
+#pragma unroll
+                for (int j = 0; j < FN; ++j) xa[j][e] = ps[row * BN + a_col0 + j * 32];
+#pragma unroll
+                for (int i = 0; i < FK; ++i) xb[i][e] = qs[row * BK + b_col0 + i * 32];
+            }
+            wg_bf16x8 ph[FN], pm[FN], pl[FN];
+#pragma unroll
+            for (int j = 0; j < FN; ++j) wg_split3(xa[j], ph[j], pm[j], pl[j]);
+#pragma unroll
+            for (int i = 0; i < FK; ++i) {
+                wg_bf16x8 qh, qm, ql;
+                wg_split3(xb[i], qh, qm, ql);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    f32x16 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm[j], c, 0, 0, 0);   // small terms first
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pl[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, ph[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pm[j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph[j], c, 0, 0, 0);
+                    acc[i][j] = c;
+                }
+                if (i == 0) issue(m_begin + (t + NBUF - 1) * WG_BM, (t + NBUF - 1) % NBUF);
+            }
+        } else {
         // the whole stage's operands up front ((FN+FK)*8 VGPRs): the reads of step ks+1.. land
         // under the MFMAs of step ks instead of a lgkmcnt(0) bubble before every step
         float fa[WG_BM / 2][FN], fb[WG_BM / 2][FK];
@@ -382,6 +432,7 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
         // all operand reads of the stage, then the MFMAs
         __builtin_amdgcn_sched_group_barrier(0x100, (WG_BM / 2) * (FN + FK), 0);
         __builtin_amdgcn_sched_group_barrier(0x008, (WG_BM / 2) * FN * FK, 0);
+        }
         // bias column sums after the MFMA block (a divergent branch here does not split it)
         if (tid < bias_w) {   // one column per thread, all rows of the stage
             const float* img = p.bias_mode == 1 ? ps : qs;
@@ -1043,7 +1094,11 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
     }
     dim3 grid(p.gx * p.gy * pl.splits);
     if (phase & 1) {
-#define PU_WG_DMA(BN_, BK_, WN_, WK_) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3>), grid, dim3(256), 0, s, p)
+#define PU_WG_DMA(BN_, BK_, WN_, WK_)                                                                    \
+    do {                                                                                                     \
+        if (a->math == 1) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, true>), grid, dim3(256), 0, s, p); \
+        else hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, false>), grid, dim3(256), 0, s, p); \
+    } while (0)
 #define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
         if (pl.dma) {
             if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);

@@ -29,14 +29,16 @@ class ConvArgs(ctypes.Structure):
                 ("weight", P), ("k_pad", c_int), ("cgroup", c_int), ("n", c_int), ("bias", P),
                 ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int),
                 ("workspace", P), ("ws_bytes", c_size),
-                ("resid", P), ("shuf_h", c_int), ("shuf_w", c_int), ("shuf_off", c_int)]
+                ("resid", P), ("shuf_h", c_int), ("shuf_w", c_int), ("shuf_off", c_int),
+                ("weight6", P)]
 
 
 class WgradArgs(ctypes.Structure):
     _fields_ = [("batch", c_int), ("in_h", c_int), ("in_w", c_int), ("out_h", c_int), ("out_w", c_int),
                 ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int),
                 ("rows", P), ("n", c_int), ("src0", P), ("c0", c_int), ("src1", P), ("c1", c_int),
-                ("bias_mode", c_int), ("dweight", P), ("dbias", P), ("accumulate", c_int)]
+                ("bias_mode", c_int), ("dweight", P), ("dbias", P), ("accumulate", c_int),
+                ("math", c_int)]
 
 
 class PlasticArgs(ctypes.Structure):
@@ -68,6 +70,7 @@ SIGNATURES = [
     ("pu_wgrad_tile", c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    ("pu_split_weight6", c_int, [P, P, c_int, c_int, P]),
     ("pu_nchw_to_nhwc", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_channel_scale", c_int, [P, P, P, c_int, c_ll, c_int, P]),
     ("pu_conv_igemm_bf16", c_int, [ctypes.POINTER(ConvArgs), P]),

@@ -4,6 +4,7 @@ Every wrapper enqueues on torch's *current* HIP stream and never synchronises.  
 fp32, contiguous and resident on the ROCm device; activations are NHWC.
 """
 import ctypes
+import os
 
 import torch
 
@@ -22,7 +23,25 @@ def lib():
 
 # ------------------------------------------------------------------------------ launch profiler
 _PROF = None
-_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct"}
+_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6"}
+
+# fp32 GEMM arithmetic of the MFMA convolutions: "split6" (default) = each fp32 product as 6 exact
+# bf16 products on the bf16 MFMA pipe (pu_split_weight6 / pu_conv_args.weight6, fp32-accurate);
+# "native" = v_mfma_f32_32x32x2_f32.  Read when a weight is packed and when a conv launches.
+_FP32_MATH = os.environ.get("PU_FP32_MATH", "split6")
+
+
+def fp32_math():
+    return _FP32_MATH
+
+
+def set_fp32_math(mode):
+    """'split6' or 'native' (tests / ablations).  Returns the previous mode."""
+    global _FP32_MATH
+    if mode not in ("split6", "native"):
+        raise ValueError("fp32 math must be 'split6' or 'native', got %r" % (mode,))
+    prev, _FP32_MATH = _FP32_MATH, mode
+    return prev
 
 
 class KernelProfiler:
@@ -139,6 +158,9 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,
                  _p(resid), shuf[0], shuf[1], shuf[2])
+    w6 = getattr(weight, "_split6", None) if (dt != BF16 and _FP32_MATH == "split6") else None
+    if w6 is not None:
+        a.weight6 = w6.data_ptr()
     L = lib()
     if dt == BF16:
         _igemm_bf16(L, a, batch, out_hw, k, c0, c1, n, dst0)
@@ -194,7 +216,7 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     _req(dweight, "dweight"); _req(dbias, "dbias")
     a = WgradArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                   _p(rows), n, _p(src0), c0, _p(src1), c1, bias_mode, _p(dweight), _p(dbias),
-                  1 if accumulate else 0)
+                  1 if accumulate else 0, 1 if (dt != BF16 and _FP32_MATH == "split6") else 0)
     L = lib()
     if dt == BF16:
         nbytes = L.pu_wgrad_bf16_workspace_bytes(ctypes.byref(a))
@@ -219,6 +241,8 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
     M = batch * out_hw[0] * out_hw[1]
     tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct")[qv.value])
+    if a.math == 1 and qv.value == 1:
+        tag = tag[:-1] + ",x6>"
     # the GEMM and the split reduction timed apart (they are separate kernels in rocprof too)
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
         check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 1, _stream()), "pu_wgrad_phase")
@@ -237,6 +261,18 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
     fn = lib().pu_pack_weight_bf16 if out.dtype == BF16 else lib().pu_pack_weight
     with _Rec("pack_weight", nbytes=4.0 * w.numel() + out.element_size() * out.numel()):
         check(fn(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, cgroup, _stream()), "pu_pack_weight")
+    if out.dtype == torch.float32 and _FP32_MATH == "split6" and k_pad % 16 == 0:
+        out._split6 = split_weight6(out)      # travels with the packed operand (igemm picks it up)
+    return out
+
+
+def split_weight6(packed):
+    """packed fp32 [n][k_pad] -> bf16 planes [k_pad/16][6][n][8] (hi/mid/lo, exact split)."""
+    _req(packed, "packed")
+    n, k_pad = packed.shape
+    out = torch.empty(k_pad // 16, 6, n, 8, dtype=BF16, device=packed.device)
+    with _Rec("pack_weight", nbytes=4.0 * packed.numel() + 6.0 * packed.numel()):
+        check(lib().pu_split_weight6(packed.data_ptr(), out.data_ptr(), n, k_pad, _stream()), "pu_split_weight6")
     return out
 
 
