@@ -249,14 +249,20 @@ def main():
             if d["bytes"]:
                 e["GB_s"] = round(d["bytes"] / (d["ms"] * 1e-3) / 1e9, 1)
             kern[tag] = e
-        peak, cu, clk = fp32_mfma_peak_tflops(K)
-        basis = "fp32 MFMA 256 FLOP/clk/CU x %d CU x %.2f GHz" % (cu, clk)
-        if args.config == "c3":     # v_mfma_f32_32x32x16_bf16: 4096 FLOP/clk/CU dense
-            peak *= 16.0
-            basis = "bf16 MFMA 4096 FLOP/clk/CU x %d CU x %.2f GHz (dense)" % (cu, clk)
+        f32peak, cu, clk = fp32_mfma_peak_tflops(K)
         mfma = {t: d for t, d in summ.items() if d["flops"] and (t.startswith("igemm") or t.startswith("wgrad"))}
         dom = max(mfma.items(), key=lambda kv: kv[1]["ms"])
         dtag, dd = dom
+        if args.config == "c3":     # v_mfma_f32_32x32x16_bf16: 4096 FLOP/clk/CU dense
+            peak = f32peak * 16.0
+            basis = "bf16 MFMA 4096 FLOP/clk/CU x %d CU x %.2f GHz (dense)" % (cu, clk)
+        elif "x6" in dtag:          # fp32 products as 6 bf16 MFMA products: 4096/6 fp32-FLOP/clk/CU
+            peak = f32peak * 16.0 / 6.0
+            basis = ("fp32 as 6 bf16 products: bf16 MFMA 4096 FLOP/clk/CU / 6 x %d CU x %.2f GHz "
+                     "(fp32-equivalent; native fp32 MFMA peak %.1f TF)" % (cu, clk, f32peak))
+        else:
+            peak = f32peak
+            basis = "fp32 MFMA 256 FLOP/clk/CU x %d CU x %.2f GHz" % (cu, clk)
         ach = dd["flops"] / (dd["ms"] * 1e-3) / 1e12
         tot_f = sum(d["flops"] for d in mfma.values())
         tot_ms = sum(d["ms"] for d in mfma.values())
@@ -303,7 +309,11 @@ def main():
             "data": "synthetic: x~U[0,1) [B,1,%d,%d], targets (U>0.5); random init (seed 0)" % (S, S),
             "config": {"workload": CONFIGS[args.config] % vars(args),
                        "global_batch": world * B, "per_gpu_batch": B, "img": S,
-                       "parallelism": "dp%d" % world if world > 1 else "single"},
+                       "parallelism": "dp%d" % world if world > 1 else "single",
+                       "fp32_gemm": None if args.config == "c3" else
+                       {"split6": "fp32 operands split exactly into 3 bf16 terms, 6 bf16 MFMA products per fp32 "
+                                  "product, fp32 accumulation (error of an fp32 product)",
+                        "native": "v_mfma_f32_32x32x2_f32"}[K.fp32_math()]},
             "final_loss": final_loss,
             "roofline": roof,
             "oja_update": oja,
