@@ -21,6 +21,8 @@
  *   pu_plastic_bwd     mm/mul/sigmoid backward         (autograd, train.py:110)
  *   pu_bce_fwd/bwd     nn.BCELoss (mean, log >= -100)  src/train.py:70,101-105
  *   pu_adam_multi      torch.optim.Adam.step           src/train.py:66,111
+ *   pu_bn_fwd/bwd      nn.BatchNorm2d (+ReLU)          src/unet/unet_p.py:186-193 (batch_norm=True)
+ *   pu_upsample_bilinear2x_fwd/bwd  nn.Upsample(2, bilinear, align_corners) unet_p.py:235-236
  *   pu_pack_weight     (layout only) OIHW parameters -> the packed GEMM operands
  *   pu_nchw_to_nhwc    (layout only) the [B,C,H,W] model input -> NHWC
  *
@@ -160,6 +162,31 @@ int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, vo
  * (partials into the workspace), phase 2 = the fixed-order reduction + scatter; 1 then 2 on the
  * same stream == pu_wgrad */
 int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, int phase, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * BatchNorm2d (+ ReLU) of double_conv(batch_norm=True)   src/unet/unet_p.py:186-193
+ *   training: slot b is normalised by its own statistics over H x W (the reference trains with
+ *   batch size 1) and the running statistics take the B per-slot updates in slot order
+ *   (running = (1-m) running + m stat, unbiased variance; NULL running buffers: no update);
+ *   save_mean / save_rstd [batch][c].  eval (training = 0): running statistics, save_* [c].
+ *   y = relu?((z - mean) * rstd * gamma + beta); gamma / beta may be NULL (affine=False).
+ * pu_bn_bwd: given g = dL/dy (ReLU mask applied), dz and dgamma / dbeta [c] (NULL: skipped).
+ * fp64 partial sums, fixed-order reduction (deterministic).  c % 4 == 0, NHWC, 16-B aligned.
+ * ------------------------------------------------------------------------------------------- */
+size_t pu_bn_workspace_bytes(int batch, long long hw, int c);
+int pu_bn_fwd(const float* z, const float* gamma, const float* beta, float* running_mean, float* running_var,
+              float* y, float* save_mean, float* save_rstd, int batch, long long hw, int c, float eps,
+              float momentum, int training, int relu, void* workspace, size_t workspace_bytes, void* stream);
+int pu_bn_bwd(const float* z, const float* g, const float* save_mean, const float* save_rstd,
+              const float* gamma, float* dz, float* dgamma, float* dbeta, int batch, long long hw, int c,
+              void* workspace, size_t workspace_bytes, void* stream);
+
+/* nn.Upsample(scale_factor=2, mode='bilinear', align_corners=True) of up(bilinear=True)
+ * src/unet/unet_p.py:235-236, NHWC x [batch][h][w][c] -> y [batch][2h][2w][c]; the backward
+ * gathers per input pixel (deterministic) and multiplies by (mask > 0) when mask != NULL. */
+int pu_upsample_bilinear2x_fwd(const float* x, float* y, int batch, int h, int w, int c, void* stream);
+int pu_upsample_bilinear2x_bwd(const float* dy, const float* mask, float* dx, int batch, int h, int w, int c,
+                               void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Layout helpers

@@ -201,6 +201,14 @@ class RefUNetp(_PlasticBase):
         self.outc = _Outconv(base_ch, n_classes)
 
     def trunk(self, x):
+        # Batched semantics with batch_norm=True: the reference trains at batch
+        # size 1, so in training mode each slot runs on its own (its own BatchNorm statistics,
+        # running statistics updated slot by slot in order).
+        if self.training and x.shape[0] > 1 and any(isinstance(m, nn.BatchNorm2d) for m in self.modules()):
+            return torch.cat([self._trunk(x[b:b + 1]) for b in range(x.shape[0])])
+        return self._trunk(x)
+
+    def _trunk(self, x):
         xs = [self.inc(x)]
         for i in range(1, self.depth):
             xs.append(getattr(self, "down%d" % i)(xs[-1]))

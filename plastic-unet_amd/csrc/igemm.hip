@@ -600,6 +600,12 @@ __device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf
 #ifndef PU_X6_NBUF
 #define PU_X6_NBUF 3
 #endif
+#ifndef PU_X6_PRIO
+#define PU_X6_PRIO 0     // s_setprio(1) around each sub-tile's MFMA cluster
+#endif
+#ifndef PU_X6_IL
+#define PU_X6_IL 0       // sched_group_barrier: interleave each MFMA with VALU/SALU work
+#endif
 
 template <int BM, int BN, int WM, int WN, int NBUF, int KSUB>
 __global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
@@ -754,6 +760,7 @@ __global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
             for (int i = 0; i < FM; ++i) {
                 bf16x8_t xh, xm, xl;
                 split3_bf16(xa[i], xb[i], xh, xm, xl);
+                if (PU_X6_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int j = 0; j < FN; ++j) {
                     f32x16 c = acc[i][j];
@@ -765,7 +772,17 @@ __global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
                     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xh, c, 0, 0, 0);
                     acc[i][j] = c;
                 }
+                if (PU_X6_PRIO) __builtin_amdgcn_s_setprio(0);
                 if (PU_X6_SCHED == 1 && u == 0 && i == 0) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
+            }
+            if (PU_X6_IL) {
+                __builtin_amdgcn_sched_group_barrier(0x100, FM * 2 + FN * 3, 0);
+#pragma unroll
+                for (int q = 0; q < FM * FN * 6; ++q) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);
+                }
             }
         }
     }

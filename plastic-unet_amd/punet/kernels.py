@@ -469,3 +469,61 @@ def adam_multi(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, weight_d
     with _Rec("adam", nbytes=28.0 * sum(p.numel() for p in params)):
         check(lib().pu_adam_multi(arr, n, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt, _stream()),
               "pu_adam_multi")
+
+
+# --------------------------------------------------------------------- BatchNorm2d / bilinear 2x
+def bn_fwd(z, gamma, beta, running_mean, running_var, eps, momentum, training, relu=True):
+    """BatchNorm2d (+ReLU) over NHWC z [B,H,W,C].  training: per-slot statistics over H x W (the
+    reference's bs=1 BatchNorm, slot by slot) and B in-order running-statistic updates; else the
+    running statistics.  Returns (y, save_mean [B,C] or [C], save_rstd)."""
+    _req(z, "z")
+    B, H, W, C = z.shape
+    y = torch.empty_like(z)
+    shape = (B, C) if training else (C,)
+    mean = torch.empty(shape, dtype=torch.float32, device=z.device)
+    rstd = torch.empty(shape, dtype=torch.float32, device=z.device)
+    L = lib()
+    nbytes = L.pu_bn_workspace_bytes(B, H * W, C)
+    ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=z.device)
+    with _Rec("batchnorm_fwd", nbytes=4.0 * (3 if training else 2) * z.numel()):
+        check(L.pu_bn_fwd(z.data_ptr(), _p(gamma), _p(beta), _p(running_mean), _p(running_var), y.data_ptr(),
+                          mean.data_ptr(), rstd.data_ptr(), B, H * W, C, float(eps), float(momentum),
+                          1 if training else 0, 1 if relu else 0, ws.data_ptr(), nbytes, _stream()), "pu_bn_fwd")
+    return y, mean, rstd
+
+
+def bn_bwd(z, g, mean, rstd, gamma, dgamma=None, dbeta=None):
+    """Backward of the training-mode BatchNorm2d given g = dL/d(BN output) (ReLU mask already
+    applied): returns dz; writes dgamma / dbeta [C] when given."""
+    _req(z, "z"); _req(g, "g")
+    B, H, W, C = z.shape
+    dz = torch.empty_like(z)
+    L = lib()
+    nbytes = L.pu_bn_workspace_bytes(B, H * W, C)
+    ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=z.device)
+    with _Rec("batchnorm_bwd", nbytes=4.0 * 5 * z.numel()):
+        check(L.pu_bn_bwd(z.data_ptr(), g.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _p(gamma), dz.data_ptr(),
+                          _p(dgamma), _p(dbeta), B, H * W, C, ws.data_ptr(), nbytes, _stream()), "pu_bn_bwd")
+    return dz
+
+
+def upsample_bilinear2x(x):
+    """nn.Upsample(scale_factor=2, mode='bilinear', align_corners=True) on NHWC x."""
+    _req(x, "x")
+    B, h, w, C = x.shape
+    y = torch.empty(B, 2 * h, 2 * w, C, dtype=torch.float32, device=x.device)
+    with _Rec("upsample_fwd", nbytes=4.0 * (x.numel() + y.numel())):
+        check(lib().pu_upsample_bilinear2x_fwd(x.data_ptr(), y.data_ptr(), B, h, w, C, _stream()),
+              "pu_upsample_bilinear2x_fwd")
+    return y
+
+
+def upsample_bilinear2x_bwd(dy, mask=None):
+    """Gradient of upsample_bilinear2x w.r.t. its input, times (mask > 0) when given."""
+    _req(dy, "dy"); _req(mask, "mask")
+    B, H2, W2, C = dy.shape
+    dx = torch.empty(B, H2 // 2, W2 // 2, C, dtype=torch.float32, device=dy.device)
+    with _Rec("upsample_bwd", nbytes=4.0 * (dy.numel() + 2 * dx.numel())):
+        check(lib().pu_upsample_bilinear2x_bwd(dy.data_ptr(), _p(mask), dx.data_ptr(), B, H2 // 2, W2 // 2, C,
+                                               _stream()), "pu_upsample_bilinear2x_bwd")
+    return dx

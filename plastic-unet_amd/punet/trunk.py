@@ -152,7 +152,16 @@ def as_nhwc_input(x):
 
 class UNetpTrunk:
     """Parameter order and kernel schedule of the generalised UNetp trunk (depth D).  Models with a
-    ``coord`` stem (CoordConvUNetp) get its w,b appended after outc and ``up_first`` concats."""
+    ``coord`` stem (CoordConvUNetp) get its w,b appended after outc and ``up_first`` concats.
+
+    Variants of the reference's constructor flags (unet_p.py:9-52):
+      batch_norm=True         (:186-193) each conv is Conv -> BatchNorm2d -> ReLU: the conv epilogue
+                              keeps bias only, punet.kernels.bn_fwd normalises slot by slot (the
+                              reference's batch size 1) and applies the ReLU; backward runs bn_bwd
+                              on the masked gradient before the conv's wgrad / dgrad
+      bilinear_upsample=True  (:235-236) nn.Upsample(2, bilinear, align_corners=True) in place of
+                              the ConvTranspose2d: no parameters, gather-form backward
+    """
 
     def __init__(self, model):
         self.depth = model.depth
@@ -162,37 +171,75 @@ class UNetpTrunk:
         # activations dtype: float32, or bfloat16 (config C3; fp32 accumulation, fp32 parameters
         # and gradients; the 1-channel stem conv runs in fp32 and its output is rounded once)
         self.dtype = getattr(model, "compute_dtype", torch.float32)
+        self.bilinear = bool(getattr(model, "bilinear_upsample", False))
+        self.training = True
         self.names = []
         self.packs = _Packs()
-        mods = {"inc": model.inc.conv.conv}
+        seqs = {"inc": model.inc.conv.conv}
         for i in range(1, self.depth):
-            mods["down%d" % i] = getattr(model, "down%d" % i).mpconv[1].conv
+            seqs["down%d" % i] = getattr(model, "down%d" % i).mpconv[1].conv
         for j in range(1, self.depth):
-            up = getattr(model, "up%d" % j)
-            mods["up%d.up" % j] = up.up
-            mods["up%d" % j] = up.conv.conv
+            seqs["up%d" % j] = getattr(model, "up%d" % j).conv.conv
         self.params = []
-        # order: inc c0 w,b, c1 w,b ; down_i ... ; up_j: up w,b, c0 w,b, c1 w,b ; outc w,b
-        for key in ["inc"] + ["down%d" % i for i in range(1, self.depth)]:
-            seq = mods[key]
-            for idx in (0, 2):
-                self.params += [seq[idx].weight, seq[idx].bias]
+        self.slot = {}           # conv key ("inc.c0", "up2.up", "outc", ...) -> index of its weight
+        self.bn = {}             # conv key -> its BatchNorm2d module
+        bn_mods = []
+
+        def add(key, w, b):
+            self.slot[key] = len(self.params)
+            self.params += [w, b]
+
+        # order: inc c0 w,b, c1 w,b ; down_i ... ; up_j: [up w,b], c0 w,b, c1 w,b ; outc w,b ;
+        # [coord w,b] ; then the BatchNorm affine parameters (w,b) in conv order
+        def add_double(name):
+            convs = [m for m in seqs[name] if isinstance(m, torch.nn.Conv2d)]
+            norms = [m for m in seqs[name] if isinstance(m, torch.nn.BatchNorm2d)]
+            for idx, cm in enumerate(convs):
+                add("%s.c%d" % (name, idx), cm.weight, cm.bias)
+                if norms:
+                    bn_mods.append(("%s.c%d" % (name, idx), norms[idx]))
+
+        add_double("inc")
+        for i in range(1, self.depth):
+            add_double("down%d" % i)
         for j in range(1, self.depth):
-            upm = mods["up%d.up" % j]
-            self.params += [upm.weight, upm.bias]
-            seq = mods["up%d" % j]
-            for idx in (0, 2):
-                self.params += [seq[idx].weight, seq[idx].bias]
-        self.params += [model.outc.conv.weight, model.outc.conv.bias]
+            upm = getattr(model, "up%d" % j).up
+            if isinstance(upm, torch.nn.ConvTranspose2d):
+                add("up%d.up" % j, upm.weight, upm.bias)
+            elif not self.bilinear:
+                raise RuntimeError("up%d.up is neither ConvTranspose2d nor bilinear" % j)
+            add_double("up%d" % j)
+        add("outc", model.outc.conv.weight, model.outc.conv.bias)
         if self.coord is not None:
-            self.params += [self.coord.conv.weight, self.coord.conv.bias]
+            add("coord", self.coord.conv.weight, self.coord.conv.bias)
+        self.n_core = len(self.params)
+        for key, m in bn_mods:
+            if m.momentum is None:
+                raise NotImplementedError("BatchNorm2d(momentum=None) (cumulative averaging) is not built")
+            self.bn[key] = m
+            self.slot[key + ".bn"] = len(self.params)
+            self.params += [m.weight, m.bias]
+        if (self.bn or self.bilinear) and self.dtype != torch.float32:
+            raise NotImplementedError("batch_norm / bilinear_upsample run in fp32 (precision='fp32')")
         self.gradbuf = None      # punet.dp.GradBuffer: backward writes grads into its views
         self.debug = None        # dict: when set, backward stores each layer's dZ (tests/diagnostics)
 
     def backward_order(self):
-        """Parameters in the order backward() completes their gradients (outc first, stem last)."""
-        core = self.params[:-2] if self.coord is not None else self.params
-        return list(reversed(core)) + (self.params[-2:] if self.coord is not None else [])
+        """Parameters in the order backward() completes their gradients (outc first, stem last;
+        each BatchNorm pair completes just before its conv)."""
+        order = []
+        core = self.params[:self.n_core]
+        if self.coord is not None:
+            core = core[:-2]
+        bn_of = {self.slot[k]: self.slot[k + ".bn"] for k in self.bn}
+        for idx in range(len(core) - 2, -2, -2):
+            if idx in bn_of:
+                j = bn_of[idx]
+                order += [self.params[j + 1], self.params[j]]
+            order += [core[idx + 1], core[idx]]
+        if self.coord is not None:
+            order += self.params[self.n_core - 2:self.n_core]
+        return order
 
     def _ready(self, i, n=2):
         """params[i:i+n]'s gradient kernels are enqueued: let an armed BucketReducer know."""
@@ -210,48 +257,87 @@ class UNetpTrunk:
         return [gb.view_for(p) for p in self.params]
 
     # -------------------------------------------------------------------------------- forward
+    def _conv(self, key, P, s, x0, x1=None):
+        """conv3x3 (+ BatchNorm) + ReLU of conv `key` over [x0 | x1]."""
+        i = self.slot[key]
+        bnm = self.bn.get(key)
+        if bnm is None:
+            return conv3x3(x0, P[i], P[i + 1], self.packs, x1=x1)
+        z = conv3x3(x0, P[i], P[i + 1], self.packs, x1=x1, relu=False)
+        j = self.slot[key + ".bn"]
+        training = self.training or not bnm.track_running_stats
+        update = self.training and bnm.track_running_stats
+        y, mean, rstd = K.bn_fwd(z, P[j], P[j + 1], bnm.running_mean if (update or not training) else None,
+                                 bnm.running_var if (update or not training) else None, bnm.eps, bnm.momentum,
+                                 training)
+        if update:
+            bnm.num_batches_tracked.add_(z.shape[0])     # one reference forward per slot
+        if s is not None:
+            s[key + ".z"] = z
+            s[key + ".stat"] = (mean, rstd)
+        return y
+
     def forward(self, x, params, save):
-        it = iter(params)
-        nxt = lambda: (next(it), next(it))  # noqa: E731
+        P = params
         D = self.depth
         pk = self.packs
         s = {"x": x}
         if self.coord is not None:     # stem: 1x1 conv + ReLU over the AddCoords input
-            cw, cb = params[-2], params[-1]
+            ci = self.slot["coord"]
+            cw, cb = P[ci], P[ci + 1]
             B, H, W, ca = x.shape
             x = torch.empty(B, H, W, cw.shape[0], dtype=torch.float32, device=cw.device)
             K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, src0=s["x"], c0=ca,
                     weight=pk.get(cw, PU_PACK_CONV_FWD, K.round16(ca)), k_pad=K.round16(ca), n=cw.shape[0],
                     bias=cb, dst0=x, relu=True)
             s["stem"] = x
-        w, b = nxt(); t = conv3x3(x, w, b, pk)
+        t = self._conv("inc.c0", P, s, x)
         if self.dtype != t.dtype:
             t = K.to_bf16(t)
         s["inc.t"] = t
-        w, b = nxt(); y = conv3x3(t, w, b, pk)
+        y = self._conv("inc.c1", P, s, t)
         skips = [y]
         for i in range(1, D):
             p = K.maxpool2_fwd(skips[-1]); s["down%d.p" % i] = p
-            w, b = nxt(); t = conv3x3(p, w, b, pk); s["down%d.t" % i] = t
-            w, b = nxt(); y = conv3x3(t, w, b, pk)
+            t = self._conv("down%d.c0" % i, P, s, p); s["down%d.t" % i] = t
+            y = self._conv("down%d.c1" % i, P, s, t)
             skips.append(y)
         s["skips"] = skips
         y = skips[-1]
         for j in range(1, D):
             skip = skips[D - 1 - j]
-            w, b = nxt(); u = convT2x2(y, w, b, pk); s["up%d.u" % j] = u
-            if self.up_first:
-                w, b = nxt(); t = conv3x3(u, w, b, pk, x1=skip)
+            if self.bilinear:
+                u = K.upsample_bilinear2x(y)
             else:
-                w, b = nxt(); t = conv3x3(skip, w, b, pk, x1=u)
+                ui = self.slot["up%d.up" % j]
+                u = convT2x2(y, P[ui], P[ui + 1], pk)
+            s["up%d.u" % j] = u
+            if self.up_first:
+                t = self._conv("up%d.c0" % j, P, s, u, skip)
+            else:
+                t = self._conv("up%d.c0" % j, P, s, skip, u)
             s["up%d.t" % j] = t
-            w, b = nxt(); y = conv3x3(t, w, b, pk)
+            y = self._conv("up%d.c1" % j, P, s, t)
             s["up%d.y" % j] = y
-        w, b = nxt()
-        logits = K.outconv_fwd(y, w.reshape(-1), b)
+        o = self.slot["outc"]
+        logits = K.outconv_fwd(y, P[o].reshape(-1), P[o + 1])
         return logits, (s if save else None)
 
     # ------------------------------------------------------------------------------- backward
+    def _bn_back(self, key, g, s, P, grads, out):
+        """g = dL/d(BN output) (ReLU mask applied) -> dL/dz of conv `key`; BatchNorm grads."""
+        if key not in self.bn:
+            return g
+        j = self.slot[key + ".bn"]
+        o = out(j)
+        mean, rstd = s[key + ".stat"]
+        dgam = torch.empty_like(P[j]) if o is None else o[0]
+        dbet = torch.empty_like(P[j + 1]) if o is None else o[1]
+        dz = K.bn_bwd(s[key + ".z"], g, mean, rstd, P[j], dgam, dbet)
+        grads[j], grads[j + 1] = dgam, dbet
+        self._ready(j)
+        return dz
+
     def backward(self, s, dlogits, params):
         D = self.depth
         pk = self.packs
@@ -259,13 +345,11 @@ class UNetpTrunk:
         grads = [None] * len(P)
         sink = self.grad_sinks()
         out = (lambda i: None) if sink is None else (lambda i: (sink[i], sink[i + 1]))  # noqa: E731
-        # parameter slots (see __init__ order)
-        n_enc = 4 * D
-        up_base = lambda j: n_enc + 6 * (j - 1)  # noqa: E731
-        outc = n_enc + 6 * (D - 1)
+        sl = self.slot
         skips = s["skips"]
 
         y_last = s["up%d.y" % (D - 1)]
+        outc = sl["outc"]
         o = out(outc)
         g, dwo, dbo = K.outconv_bwd(y_last, P[outc].reshape(-1), dlogits, relu_mask=True,
                                     out=None if o is None else (o[0].view(-1), o[1]))
@@ -275,68 +359,78 @@ class UNetpTrunk:
 
         gskip = [None] * (D - 1)
         for j in range(D - 1, 0, -1):
-            base = up_base(j)
+            c0, c1 = sl["up%d.c0" % j], sl["up%d.c1" % j]
             t = s["up%d.t" % j]
             u = s["up%d.u" % j]
             skip = skips[D - 1 - j]
             y_prev = skips[D - 1] if j == 1 else s["up%d.y" % (j - 1)]
             if self.debug is not None:
                 self.debug["up%d.c1" % j] = g
-            # conv1 of up_j: y_j = relu(conv(t));  g = dZ
-            grads[base + 4], grads[base + 5] = conv3x3_wgrad(g, t, out=out(base + 4))
-            self._ready(base + 4)
-            dt, _ = conv3x3_dgrad(g, P[base + 4], pk, mask0=t)
+            # conv1 of up_j: y_j = relu([bn](conv(t)));  g = dL/d(pre-ReLU)
+            g = self._bn_back("up%d.c1" % j, g, s, P, grads, out)
+            grads[c1], grads[c1 + 1] = conv3x3_wgrad(g, t, out=out(c1))
+            self._ready(c1)
+            dt, _ = conv3x3_dgrad(g, P[c1], pk, mask0=t)
+            dt = self._bn_back("up%d.c0" % j, dt, s, P, grads, out)
             # conv0 over [skip | u]  (up_first: [u | skip])
             if self.up_first:
-                grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, u, skip, out=out(base + 2))
-                self._ready(base + 2)
-                du, dskip = conv3x3_dgrad(dt, P[base + 2], pk, split=u.shape[3], mask1=skip)
+                grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, u, skip, out=out(c0))
+                self._ready(c0)
+                du, dskip = conv3x3_dgrad(dt, P[c0], pk, split=u.shape[3], mask1=skip)
             else:
-                grads[base + 2], grads[base + 3] = conv3x3_wgrad(dt, skip, u, out=out(base + 2))
-                self._ready(base + 2)
-                dskip, du = conv3x3_dgrad(dt, P[base + 2], pk, split=skip.shape[3], mask0=skip)
+                grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, skip, u, out=out(c0))
+                self._ready(c0)
+                dskip, du = conv3x3_dgrad(dt, P[c0], pk, split=skip.shape[3], mask0=skip)
             if self.debug is not None:
                 self.debug["up%d.c0" % j] = dt
                 self.debug["up%d.up" % j] = du
             gskip[D - 1 - j] = dskip
-            # ConvT
-            grads[base], grads[base + 1] = convT2x2_wgrad(y_prev, du, out=out(base))
-            self._ready(base)
-            g = convT2x2_dgrad(du, P[base], pk, mask=y_prev)
+            if self.bilinear:
+                g = K.upsample_bilinear2x_bwd(du, mask=y_prev)
+            else:
+                ui = sl["up%d.up" % j]
+                grads[ui], grads[ui + 1] = convT2x2_wgrad(y_prev, du, out=out(ui))
+                self._ready(ui)
+                g = convT2x2_dgrad(du, P[ui], pk, mask=y_prev)
 
         for i in range(D - 1, 0, -1):
-            base = 4 * i
+            c0, c1 = sl["down%d.c0" % i], sl["down%d.c1" % i]
             t = s["down%d.t" % i]
             p = s["down%d.p" % i]
             if self.debug is not None:
                 self.debug["down%d.c1" % i] = g
-            grads[base + 2], grads[base + 3] = conv3x3_wgrad(g, t, out=out(base + 2))
-            self._ready(base + 2)
-            dt, _ = conv3x3_dgrad(g, P[base + 2], pk, mask0=t)
-            grads[base], grads[base + 1] = conv3x3_wgrad(dt, p, out=out(base))
-            self._ready(base)
+            g = self._bn_back("down%d.c1" % i, g, s, P, grads, out)
+            grads[c1], grads[c1 + 1] = conv3x3_wgrad(g, t, out=out(c1))
+            self._ready(c1)
+            dt, _ = conv3x3_dgrad(g, P[c1], pk, mask0=t)
+            dt = self._bn_back("down%d.c0" % i, dt, s, P, grads, out)
+            grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, p, out=out(c0))
+            self._ready(c0)
             if self.debug is not None:
                 self.debug["down%d.c0" % i] = dt
-            dp, _ = conv3x3_dgrad(dt, P[base], pk)
+            dp, _ = conv3x3_dgrad(dt, P[c0], pk)
             g = K.maxpool2_bwd(skips[i - 1], dp, gskip[i - 1], relu_mask=True, accumulate=True)
 
         t = s["inc.t"]
+        c0, c1 = sl["inc.c0"], sl["inc.c1"]
         if self.debug is not None:
             self.debug["inc.c1"] = g
-        grads[2], grads[3] = conv3x3_wgrad(g, t, out=out(2))
-        self._ready(2)
-        dt, _ = conv3x3_dgrad(g, P[2], pk, mask0=t)
+        g = self._bn_back("inc.c1", g, s, P, grads, out)
+        grads[c1], grads[c1 + 1] = conv3x3_wgrad(g, t, out=out(c1))
+        self._ready(c1)
+        dt, _ = conv3x3_dgrad(g, P[c1], pk, mask0=t)
         x0 = s["stem"] if self.coord is not None else s["x"]
         if dt.dtype != x0.dtype:       # bf16 trunk: the fp32 stem's weight gradient
             dt = K.to_f32(dt)
-        grads[0], grads[1] = conv3x3_wgrad(dt, x0, out=out(0))
-        self._ready(0)
+        dt = self._bn_back("inc.c0", dt, s, P, grads, out)
+        grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, x0, out=out(c0))
+        self._ready(c0)
         if self.debug is not None:
             self.debug["inc.c0"] = dt
         if self.coord is not None:     # stem 1x1 conv: dgrad of inc.c0 (masked by the stem ReLU) + wgrad
-            dstem, _ = conv3x3_dgrad(dt, P[0], pk, mask0=x0)
+            dstem, _ = conv3x3_dgrad(dt, P[c0], pk, mask0=x0)
             B, H, W, ca = s["x"].shape
-            cs = len(P) - 2
+            cs = sl["coord"]
             o = out(cs)
             dw = torch.empty(P[cs].shape, dtype=torch.float32, device=dt.device) if o is None else o[0]
             db = torch.empty(P[cs + 1].shape, dtype=torch.float32, device=dt.device) if o is None else o[1]

@@ -97,6 +97,7 @@ class CoordConvUNetp(nn.Module):
         from punet.trunk import TrunkFunction
         from punet.head import PlasticHeadFunction, RULES
         trunk = self._trunk_plan()
+        trunk.training = self.training
         params = trunk.params
         save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         logits = TrunkFunction.apply(trunk, save, x, *params)

@@ -138,9 +138,8 @@ class UNetp(nn.Module):
             raise ValueError("Must select one learning rule ('hebb' or 'oja')")
         _check_gpu_tensor(x, "x")
         _check_gpu_tensor(hebb, "hebb")
-        if self.batch_norm or self.bilinear_upsample:
-            raise NotImplementedError("UNetp(batch_norm=True / bilinear_upsample=True) is not built on the "
-                                      "MI355X path yet")
+        if (self.batch_norm or self.bilinear_upsample) and self.precision != "fp32":
+            raise NotImplementedError("UNetp(batch_norm=True / bilinear_upsample=True) runs with precision='fp32'")
         if self.n_classes != 1:
             raise RuntimeError("the plastic head needs n_classes == 1 (activin = x.view(nbf, nbf))")
         B, C, Hh, Ww = x.shape
@@ -159,6 +158,7 @@ class UNetp(nn.Module):
         from punet.trunk import TrunkFunction
         from punet.head import PlasticHeadFunction, RULES
         trunk = self._trunk_plan()
+        trunk.training = self.training      # BatchNorm: per-slot batch statistics vs running statistics
         params = trunk.params
         save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         logits = TrunkFunction.apply(trunk, save, x, *params)

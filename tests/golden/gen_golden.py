@@ -19,6 +19,8 @@ Fixtures (each < 2 MB):
   bce_edge.npz                   BCELoss clamp edge cases (S9)
   train_capture.npz              reference train() for 2 epochs (losses, eval, final params)
   metrics.npz                    fast_iou_metric and RLE encode on fixed masks
+  unetp_{bn,bilinear,bn_bilinear}.npz  UNetp(batch_norm / bilinear_upsample) at 64x64: init, two
+                                 train-mode forwards (running statistics), grads, eval forward
 """
 import os
 import sys
@@ -151,6 +153,36 @@ def gen_unetp_c8():
         sch.step()
     save("unetp_c8_adam.npz", xs=t2n(xs[1:]), ts=t2n(ts[1:]), losses=np.array(losses, np.float64),
          hebb=t2n(hebb), **sd_arrays(net, "p."))
+
+
+def gen_variants():
+    """Reference UNetp with its constructor flags batch_norm=True / bilinear_upsample=True
+    (unet_p.py:186-193, :235-236), reference topology (base 8) at 64x64: init state, two
+    train-mode forwards (the running statistics after each), fwd/bwd grads of the first, and an
+    eval-mode forward with the updated running statistics."""
+    N = 64
+    for tag, bn, bil in (("bn", True, False), ("bilinear", False, True), ("bn_bilinear", True, True)):
+        torch.manual_seed(5)
+        net = UNetp(1, 1, CPU, rule="oja", nbf=N, batch_norm=bn, bilinear_upsample=bil)
+        init = sd_arrays(net, "p.")
+        g = torch.Generator().manual_seed(21)
+        xs = torch.rand(3, 1, 1, N, N, generator=g)
+        t0 = (torch.rand(N, N, generator=g) > 0.5).float()
+        hebb0 = 0.1 * torch.randn(N, N, generator=g)
+        net.train()
+        y, hn = net(xs[0], hebb0)
+        loss = nn.BCELoss()(y.view(-1), t0.view(-1))
+        loss.backward()
+        bufs = lambda pre: {k: v for k, v in sd_arrays(net, pre).items() if "running" in k or "num_batches" in k}  # noqa
+        after1 = bufs("s1.")
+        with torch.no_grad():
+            y2, _ = net(xs[1], hebb0)
+        after2 = bufs("s2.")
+        net.eval()
+        with torch.no_grad():
+            ye, he = net(xs[2], torch.zeros(N, N))
+        save("unetp_%s.npz" % tag, xs=t2n(xs), t=t2n(t0), hebb=t2n(hebb0), Y=t2n(y), Hn=t2n(hn), loss=t2n(loss),
+             Y2=t2n(y2), Ye=t2n(ye), He=t2n(he), **init, **after1, **after2, **grad_arrays(net, "g."))
 
 
 def trunk_from_blocks(base, depth, nbf, rule, seed):
@@ -410,6 +442,11 @@ def gen_metrics():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:          # e.g. gen_golden.py gen_variants
+        for fn in sys.argv[1:]:
+            globals()[fn]()
+        sys.exit(0)
+    gen_variants()
     gen_head()
     gen_trace_seq()
     gen_unetp_c8()

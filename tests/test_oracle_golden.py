@@ -215,3 +215,69 @@ def test_add_coords_closed_form():
     assert torch.allclose(out[0, 1, 3], torch.tensor([-1.0, -0.5, 0.0, 0.5, 1.0]))
     assert torch.allclose(out[0, 2, :, 2], torch.tensor([-1.0, -0.5, 0.0, 0.5, 1.0]))
     assert torch.allclose(out[1, 3, 0, 0], torch.tensor(np.sqrt(2 * 1.5 ** 2), dtype=torch.float32))
+
+
+@pytest.mark.parametrize("tag,bn,bil", [("bn", True, False), ("bilinear", False, True), ("bn_bilinear", True, True)])
+def test_unetp_variants_fixture(tag, bn, bil):
+    """UNetp(batch_norm / bilinear_upsample): init RNG order, train-mode fwd/bwd, the running
+    statistics after two forwards, and the eval-mode forward (reference, unet_p.py:186-193, :235-236)."""
+    g = golden("unetp_%s.npz" % tag)
+    torch.manual_seed(5)
+    net = oracle.RefUNetp(1, 1, rule="oja", nbf=64, batch_norm=bn, bilinear_upsample=bil)
+    for k, v in net.state_dict().items():
+        np.testing.assert_array_equal(v.numpy(), g["p." + k])
+    net.train()
+    xs = _t(g["xs"])
+    y, hn = net(xs[0], _t(g["hebb"]))
+    loss = oracle.bce_loss(y, _t(g["t"]))
+    loss.backward()
+    close(y, g["Y"])
+    close(hn, g["Hn"])
+    close(loss, g["loss"])
+    for k, p in net.named_parameters():
+        if p.grad is None:
+            assert k == "eta"
+            continue
+        close(p.grad, g["g." + k], rtol=1e-4, atol=1e-7)
+    sd = net.state_dict()
+    for k in sd:
+        if "s1." + k in g:
+            close(sd[k], g["s1." + k])
+    with torch.no_grad():
+        y2, _ = net(xs[1], _t(g["hebb"]))
+    close(y2, g["Y2"])
+    sd = net.state_dict()
+    nbuf = 0
+    for k in sd:
+        if "s2." + k in g:
+            close(sd[k], g["s2." + k])
+            nbuf += 1
+    assert nbuf == (3 * 18 if bn else 0)      # 18 BatchNorm2d layers x (mean, var, count)
+    net.eval()
+    with torch.no_grad():
+        ye, he = net(xs[2], torch.zeros(64, 64))
+    close(ye, g["Ye"])
+    close(he, g["He"])
+
+
+def test_unetp_bn_batched_slots_equal_sequential():
+    """Two slots in one training-mode forward == two sequential bs=1 forwards (per-slot
+    statistics; running statistics updated in slot order)."""
+    g = golden("unetp_bn.npz")
+    a = oracle.RefUNetp(1, 1, rule="oja", nbf=64, batch_norm=True)
+    _load(a, g)
+    b = oracle.RefUNetp(1, 1, rule="oja", nbf=64, batch_norm=True)
+    _load(b, g)
+    xs = _t(g["xs"])[:2, 0]
+    H = torch.stack([_t(g["hebb"])] * 2)
+    with torch.no_grad():
+        yb, _ = a(xs, H)
+        y0, _ = b(xs[0:1], H[0])
+        y1, _ = b(xs[1:2], H[1])
+    close(yb[0], y0, rtol=0, atol=0)
+    close(yb[1], y1, rtol=0, atol=0)
+    for k, v in a.state_dict().items():
+        close(v, b.state_dict()[k], rtol=0, atol=0)
+    for k in a.state_dict():
+        if "s2." + k in g:
+            close(a.state_dict()[k], g["s2." + k])

@@ -1,0 +1,187 @@
+"""UNetp(batch_norm=True / bilinear_upsample=True) on the HIP path (norm.hip + punet.trunk):
+kernel parity against PyTorch-CPU fp32, model parity against the reference's golden vectors
+(tests/golden/unetp_{bn,bilinear,bn_bilinear}.npz) and the per-slot batched BatchNorm semantics
+against the CPU oracle (oracle/ref_cpu.py)."""
+import re
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from punet import kernels as K  # noqa: E402
+from punet import bce_loss  # noqa: E402
+from unet import UNetp  # noqa: E402
+import oracle  # noqa: E402
+from conftest import golden  # noqa: E402
+
+DEV = torch.device("cuda")
+
+
+def _t(a):
+    return torch.from_numpy(np.asarray(a))
+
+
+def assert_close(got, ref, rtol=1e-4, atol_rel=1e-5):
+    got = got.detach().float().cpu()
+    ref = torch.as_tensor(ref).detach().float().cpu()
+    scale = max(ref.abs().max().item(), 1e-30)
+    torch.testing.assert_close(got, ref.reshape(got.shape), rtol=rtol, atol=atol_rel * scale)
+
+
+def check_param_grad(name, got, ref, bn, weight_grad):
+    """A conv bias followed by BatchNorm has an exactly-zero true gradient (BN removes the
+    mean): both sides hold rounding noise, so check it is noise-sized against the conv's weight
+    gradient instead of comparing the noise."""
+    if bn and re.search(r"\.conv\.[03]\.bias$", name):
+        lim = 1e-5 * float(torch.as_tensor(weight_grad).abs().max())
+        assert float(got.detach().abs().max()) <= lim and float(torch.as_tensor(ref).abs().max()) <= lim
+        return
+    assert_close(got, ref, rtol=1e-3, atol_rel=1e-4)
+
+
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 16, 16, 8), (3, 32, 32, 64), (1, 8, 12, 128)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_batchnorm_train_per_slot(B, H, W, C, relu):
+    """bn_fwd (training) == BatchNorm2d on each slot alone, running statistics after B in-order
+    updates; bn_bwd == autograd of the same."""
+    g = torch.Generator().manual_seed(B * 100 + C)
+    z = (torch.randn(B, C, H, W, generator=g) * 2 + 0.5)
+    gam = torch.rand(C, generator=g) + 0.5
+    bet = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(B, C, H, W, generator=g)
+    bn = torch.nn.BatchNorm2d(C)
+    with torch.no_grad():
+        bn.weight.copy_(gam)
+        bn.bias.copy_(bet)
+        bn.running_mean.copy_(torch.randn(C, generator=g))
+        bn.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    zr = z.clone().requires_grad_(True)
+    outs = []
+    for b in range(B):
+        o = bn(zr[b:b + 1])
+        outs.append(F.relu(o) if relu else o)
+    ref = torch.cat(outs)
+    (ref * dy).sum().backward()
+    zd = nhwc(z).to(DEV)
+    rm, rv = rm0.to(DEV), rv0.to(DEV)
+    gd, bd = gam.to(DEV), bet.to(DEV)
+    y, mean, rstd = K.bn_fwd(zd, gd, bd, rm, rv, 1e-5, 0.1, True, relu=relu)
+    assert_close(y, nhwc(ref.detach()))
+    assert_close(rm, bn.running_mean)
+    assert_close(rv, bn.running_var)
+    gin = nhwc(dy).to(DEV)
+    if relu:
+        gin = gin * (y > 0)
+    dgam = torch.empty(C, device=DEV)
+    dbet = torch.empty(C, device=DEV)
+    dz = K.bn_bwd(zd, gin, mean, rstd, gd, dgam, dbet)
+    assert_close(dz, nhwc(zr.grad), rtol=1e-4, atol_rel=1e-4)
+    assert_close(dgam, bn.weight.grad, rtol=1e-4, atol_rel=1e-5)
+    assert_close(dbet, bn.bias.grad, rtol=1e-4, atol_rel=1e-5)
+
+
+def test_batchnorm_eval_uses_running_stats():
+    g = torch.Generator().manual_seed(3)
+    B, C, H, W = 2, 16, 8, 8
+    z = torch.randn(B, C, H, W, generator=g)
+    bn = torch.nn.BatchNorm2d(C).eval()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g))
+        bn.running_mean.copy_(torch.randn(C, generator=g))
+        bn.running_var.copy_(torch.rand(C, generator=g) + 0.5)
+        ref = F.relu(bn(z))
+    y, _, _ = K.bn_fwd(nhwc(z).to(DEV), bn.weight.to(DEV), bn.bias.to(DEV), bn.running_mean.to(DEV),
+                       bn.running_var.to(DEV), bn.eps, 0.1, False)
+    assert_close(y, nhwc(ref))
+
+
+@pytest.mark.parametrize("B,h,w,C", [(2, 4, 4, 8), (1, 5, 7, 16), (3, 32, 32, 64), (2, 64, 64, 4)])
+def test_bilinear_upsample_fwd_bwd(B, h, w, C):
+    g = torch.Generator().manual_seed(h * w + C)
+    x = torch.randn(B, C, h, w, generator=g).requires_grad_(True)
+    y = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
+    dy = torch.randn(y.shape, generator=g)
+    (y * dy).sum().backward()
+    mask = (torch.rand(B, C, h, w, generator=g) > 0.3).float()
+    yd = K.upsample_bilinear2x(nhwc(x.detach()).to(DEV))
+    assert_close(yd, nhwc(y.detach()), rtol=1e-5, atol_rel=1e-6)
+    # backward: up to 16 terms per input pixel summed in another order than ATen's scatter
+    dx = K.upsample_bilinear2x_bwd(nhwc(dy).to(DEV))
+    assert_close(dx, nhwc(x.grad), rtol=1e-5, atol_rel=1e-5)
+    dxm = K.upsample_bilinear2x_bwd(nhwc(dy).to(DEV), mask=nhwc(mask).to(DEV))
+    assert_close(dxm, nhwc(x.grad * mask), rtol=1e-5, atol_rel=1e-5)
+
+
+@pytest.mark.parametrize("tag,bn,bil", [("bn", True, False), ("bilinear", False, True), ("bn_bilinear", True, True)])
+def test_unetp_variants_golden(tag, bn, bil):
+    """The product UNetp against the reference's own outputs: train-mode fwd/bwd, running
+    statistics after two forwards, eval-mode forward."""
+    g = golden("unetp_%s.npz" % tag)
+    net = UNetp(1, 1, DEV, rule="oja", nbf=64, batch_norm=bn, bilinear_upsample=bil)
+    net.load_state_dict({k[2:]: _t(v) for k, v in g.items() if k.startswith("p.")})
+    net.train()
+    xs = _t(g["xs"]).to(DEV)
+    y, hn = net(xs[0], _t(g["hebb"]).to(DEV))
+    loss = bce_loss(y, _t(g["t"]).to(DEV))
+    loss.backward()
+    assert_close(y, g["Y"])
+    assert_close(hn, g["Hn"])
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    for k, p in net.named_parameters():
+        if k == "eta":
+            assert p.grad is None
+            continue
+        check_param_grad(k, p.grad, g["g." + k], bn, g.get("g." + k.replace(".bias", ".weight")))
+    sd = net.state_dict()
+    for k in sd:
+        if "s1." + k in g:
+            assert_close(sd[k], g["s1." + k])
+    with torch.no_grad():
+        y2, _ = net(xs[1], _t(g["hebb"]).to(DEV))
+    assert_close(y2, g["Y2"])
+    sd = net.state_dict()
+    for k in sd:
+        if "s2." + k in g:
+            assert_close(sd[k], g["s2." + k])
+    net.eval()
+    with torch.no_grad():
+        ye, he = net(xs[2], torch.zeros(64, 64, device=DEV))
+    assert_close(ye, g["Ye"])
+    assert_close(he, g["He"])
+
+
+def test_unetp_bn_batched_slots_match_oracle():
+    """B slots in one training step == the oracle's per-slot BatchNorm (the reference at bs=1,
+    slot by slot): outputs, traces, running statistics and the batch-mean gradients."""
+    torch.manual_seed(9)
+    ref = oracle.RefUNetp(1, 1, rule="hebb", nbf=32, batch_norm=True, depth=4, base_ch=16)
+    net = UNetp(1, 1, DEV, rule="hebb", nbf=32, batch_norm=True, depth=4, base_ch=16)
+    net.load_state_dict(ref.state_dict())
+    g = torch.Generator().manual_seed(4)
+    B = 3
+    x = torch.rand(B, 1, 32, 32, generator=g)
+    t = (torch.rand(B, 32, 32, generator=g) > 0.5).float()
+    H = 0.1 * torch.randn(B, 32, 32, generator=g)
+    yr, hr = ref(x, H)
+    oracle.bce_loss(yr, t).backward()
+    y, h = net(x.to(DEV), H.to(DEV))
+    bce_loss(y, t.to(DEV)).backward()
+    assert_close(y, yr)
+    assert_close(h, hr)
+    rsd = ref.state_dict()
+    for k, v in net.state_dict().items():
+        assert_close(v, rsd[k])
+    rp = dict(ref.named_parameters())
+    for k, p in net.named_parameters():
+        if k == "eta":
+            continue
+        check_param_grad(k, p.grad, rp[k].grad, True, rp[k.replace(".bias", ".weight")].grad)
