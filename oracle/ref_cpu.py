@@ -28,7 +28,7 @@ import torch.nn.functional as F
 
 __all__ = [
     "unetp_channels", "RefUNetp", "RefUNetpRes", "RefCoordConvUNetp", "plastic_head",
-    "trace_update", "bce_loss", "add_coords", "ref_train_step", "ref_adam", "ref_steplr",
+    "trace_update", "plastic_head_sequential", "bce_loss", "add_coords", "ref_train_step", "ref_adam", "ref_steplr",
     "fast_iou_metric", "rle_encode_mask", "det_init_", "ref_eval_net", "ref_train_loop",
 ]
 
@@ -62,6 +62,20 @@ def plastic_head(X, H, w, alpha, eta, rule="hebb", alfa_type="free"):
     Y = torch.sigmoid(torch.matmul(X, weff))
     Hn = trace_update(H, X[:, 0, :], Y[:, 0, :], eta, rule)
     return Y, Hn
+
+
+def plastic_head_sequential(X, H, w, alpha, eta, rule="hebb", alfa_type="free"):
+    """``--hebb-mode sequential``: ONE trace threaded through the B samples in order, each sample
+    seeing the trace its predecessor left, as B successive reference calls (train.py:91-99) with
+    the same parameters.  X [B,N,N], H [N,N] -> Y [B,N,N], H' [N,N].  The trace stays detached
+    between samples (train.py:99), so sample b's head sees H_b as a constant."""
+    Ys = []
+    h = H
+    for b in range(X.shape[0]):
+        y, hn = plastic_head(X[b:b + 1], h.detach().unsqueeze(0), w, alpha, eta, rule, alfa_type)
+        Ys.append(y)
+        h = hn[0]
+    return torch.cat(Ys), h
 
 
 def bce_loss(y, t):
@@ -165,10 +179,16 @@ def _head_params(module, nbf, device=None):
 
 
 class _PlasticBase(nn.Module):
+    hebb_mode = "slots"
+
     def _head(self, logits, hebb):
         nbf = self.nbf
         B = logits.shape[0]
         X = logits.reshape(B, nbf, nbf)  # view(nbf, nbf): S7 - N must equal H and W, n_classes 1
+        if self.hebb_mode == "sequential":
+            if hebb.dim() != 2:
+                raise ValueError("hebb_mode='sequential' threads one [nbf,nbf] trace through the batch")
+            return plastic_head_sequential(X, hebb, self.w, self.alpha, self.eta, self.rule, self.alfa_type)
         single = hebb.dim() == 2
         H = hebb.unsqueeze(0) if single else hebb
         if H.shape[0] != B:
@@ -218,7 +238,7 @@ class RefUNetp(_PlasticBase):
         return self.outc(y)
 
     def forward(self, x, hebb):
-        if hebb.dim() == 2 and x.shape[0] != 1:
+        if hebb.dim() == 2 and x.shape[0] != 1 and self.hebb_mode != "sequential":
             raise ValueError("Only batch size: 1 is supported, but was: %d" % x.shape[0])
         return self._head(self.trunk(x), hebb)
 

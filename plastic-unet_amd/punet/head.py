@@ -54,6 +54,55 @@ class PlasticHeadFunction(torch.autograd.Function):
                 None, None, None, None)
 
 
+class SequentialHeadFunction(torch.autograd.Function):
+    """hebb_mode='sequential': (X [B,N,N], H [N,N], w, alpha, eta) -> (Y [B,N,N], H' [N,N]).
+
+    One trace threaded through the samples in order - B successive reference calls
+    (src/train.py:91-99) sharing the parameters: sample b runs the fused head kernel on the trace
+    sample b-1 left.  The traces are detached between samples (train.py:99), so the backward is
+    the batched head backward with the per-sample traces H_b as constants (one launch)."""
+
+    @staticmethod
+    def forward(ctx, X, H, w, alpha, eta, rule, sink=None):
+        ctx.sink = sink
+        X = X.contiguous()
+        B, N, _ = X.shape
+        Hs = torch.empty(B, N, N, dtype=torch.float32, device=X.device)
+        Y = torch.empty_like(X)
+        h = H.detach().reshape(1, N, N).contiguous()
+        wd, ad, ed = w.detach(), alpha.detach(), eta.detach()
+        for b in range(B):
+            Hs[b].copy_(h[0])
+            y, h = K.plastic_fwd(X[b:b + 1], h, wd, ad, ed, rule, True)
+            Y[b].copy_(y[0])
+        ctx.save_for_backward(X, Hs, wd, ad, Y)
+        ctx.set_materialize_grads(False)
+        hn = h.reshape(N, N)
+        ctx.mark_non_differentiable(hn)
+        return Y, hn
+
+    @staticmethod
+    def backward(ctx, dy, dhn):
+        if dhn is not None:
+            raise RuntimeError("backpropagation through the updated plastic trace is not supported: the "
+                               "reference detaches it before reuse (src/train.py:99)")
+        if dy is None:
+            return (None,) * 7
+        X, Hs, w, alpha, y = ctx.saved_tensors
+        out = None
+        if ctx.sink is not None:
+            gb, wp, ap = ctx.sink
+            if wp.grad is None and ap.grad is None:
+                out = (gb.view_for(wp), gb.view_for(ap))
+        need_dw = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dx, dw, da = K.plastic_bwd(X, Hs, w, alpha, y, dy.contiguous(), need_dx=ctx.needs_input_grad[0],
+                                   need_dw=need_dw, out=out)
+        if out is not None:
+            ctx.sink[0].ready(ctx.sink[1], ctx.sink[2])
+        return (dx, None, dw if ctx.needs_input_grad[2] else None, da if ctx.needs_input_grad[3] else None,
+                None, None, None)
+
+
 class BCELossFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, t):

@@ -5,6 +5,8 @@ per-epoch structure (train.py:78-211): zero the plastic trace each epoch (:88), 
 (forward -> BCELoss -> backward -> Adam -> StepLR, :91-112), validate with a zero trace (:131-147),
 save checkpoints (:153-203).  Differences, all opt-in:
   --batch-size B   B slots per step with per-slot traces (B=1 is the reference's loop exactly)
+  --hebb-mode sequential   one trace threaded through the B samples of each step in order
+  --batch-norm / --bilinear  the reference constructor flags batch_norm / bilinear_upsample
   --model-type     unetpres (reference default) | unetp, with --depth/--base-ch for UNetp
   --synthetic N / --dataset FILE.npz   input data (the TGS PNG loader needs skimage, absent here)
 Data-parallel training: launch with torch.distributed.run; each rank trains its contiguous shard
@@ -65,15 +67,20 @@ def train(net, X_train, X_val, y_train, y_val, params):
     for epoch in range(params["epochs"]):
         net.train()
         epoch_start_time = time.time()
-        hebb = net.initialZeroHebb(bs)                 # trace reset per epoch (train.py:88)
+        seq = getattr(net, "hebb_mode", "slots") == "sequential"
+        # trace reset per epoch (train.py:88): per-slot traces, or one trace threaded through
+        hebb = net.initialZeroHebb() if seq else net.initialZeroHebb(bs)
         losses_dev = []
         for lo, hi in _batches(samples_count, bs, world, rank):
             x = X_dev[lo:hi]
             t = Y_dev[lo:hi].reshape(hi - lo, -1)
-            h = hebb[: hi - lo]
-            loss, h = trainer.step(x, t, h)
-            if hi - lo == bs:
-                hebb = h
+            if seq:
+                loss, hebb = trainer.step(x, t, hebb)
+            else:
+                h = hebb[: hi - lo]
+                loss, h = trainer.step(x, t, h)
+                if hi - lo == bs:
+                    hebb = h
             losses_dev.append(loss)
         # one host sync per epoch instead of loss.item() per sample (train.py:106)
         epoch_losses = torch.stack(losses_dev).cpu().tolist() if losses_dev else []
@@ -119,7 +126,8 @@ def train(net, X_train, X_val, y_train, y_val, params):
 def start_train(x_train, x_valid, y_train, y_valid, out_dir, model, img_width, img_height, img_chan,
                 max_train_time=-1, load=False, gpu=True, epochs=5, lr=3e-5, val_ratio=0.05, val_every=50,
                 save_every=100, gamma=0.666, steplr=1e6, rollout=50000, prule="hebb", debug=False,
-                model_type="unetpres", depth=5, base_ch=8, neurons=16, batch_size=1):
+                model_type="unetpres", depth=5, base_ch=8, neurons=16, batch_size=1, hebb_mode="slots",
+                batch_norm=False, bilinear_upsample=False):
     world, rank, local = dp.init_from_env()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
@@ -129,11 +137,13 @@ def start_train(x_train, x_valid, y_train, y_valid, out_dir, model, img_width, i
               "gamma": gamma, "steplr": steplr, "prule": prule, "im_width": img_width, "im_height": img_height,
               "im_chan": img_chan, "debug": debug, "batch_size": batch_size}
     if model_type == "unetp":
-        net = UNetp(n_channels=img_chan, n_classes=1, nbf=img_width, batch_norm=False, bilinear_upsample=False,
-                    device=device, rule=prule, depth=depth, base_ch=base_ch)
+        net = UNetp(n_channels=img_chan, n_classes=1, nbf=img_width, batch_norm=batch_norm,
+                    bilinear_upsample=bilinear_upsample, device=device, rule=prule, depth=depth, base_ch=base_ch,
+                    hebb_mode=hebb_mode)
     else:
-        net = UNetpRes(n_channels=img_chan, n_classes=1, nbf=img_width, batch_norm=False, bilinear_upsample=False,
-                       device=device, rule=prule, neurons=neurons)
+        net = UNetpRes(n_channels=img_chan, n_classes=1, nbf=img_width, batch_norm=batch_norm,
+                       bilinear_upsample=bilinear_upsample, device=device, rule=prule, neurons=neurons,
+                       hebb_mode=hebb_mode)
     if load:
         net.load_state_dict(torch.load(model, weights_only=True))
         net.to(device)
@@ -173,6 +183,10 @@ def parse_args(argv=None):
     parser.add_option('--img-size', dest='img_size', type='int', default=101)
     parser.add_option('--batch-size', dest='batch_size', type='int', default=1)
     parser.add_option('--synthetic', dest='synthetic', type='int', default=0, help='N synthetic samples')
+    parser.add_option('--hebb-mode', dest='hebb_mode', default='slots',
+                      help="slots: one trace per batch slot; sequential: one trace threaded through the batch")
+    parser.add_option('--batch-norm', dest='batch_norm', action='store_true', default=False)
+    parser.add_option('--bilinear', dest='bilinear', action='store_true', default=False)
     parser.add_option('--seed', dest='seed', type='int', default=0)
     (options, args) = parser.parse_args(argv)
     return options
@@ -205,4 +219,5 @@ if __name__ == '__main__':
                 save_every=args.save_every, val_every=args.validate_every, rollout=args.rollout_every,
                 prule=args.prule, img_width=args.img_size, img_height=args.img_size, img_chan=1,
                 debug=args.debug, model_type=args.model_type, depth=args.depth, base_ch=args.base_ch,
-                neurons=args.neurons, batch_size=args.batch_size)
+                neurons=args.neurons, batch_size=args.batch_size, hebb_mode=args.hebb_mode,
+                batch_norm=args.batch_norm, bilinear_upsample=args.bilinear)

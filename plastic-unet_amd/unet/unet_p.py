@@ -11,6 +11,11 @@ Extensions (keyword-only in spirit, defaults reproduce the reference):
   depth=5, base_ch=8      generalised trunk width/depth (config C2 = depth 5, base 64)
   forward(x [B,C,N,N], hebb [B,N,N]) batches B independent per-slot traces; with hebb [N,N] the
   reference rule "batch size must be 1" applies unchanged.
+  hebb_mode='sequential'  one [nbf,nbf] trace threaded through the B samples of a batch in order
+                          (forward(x [B,...], hebb [nbf,nbf]) -> (Y [B,nbf,nbf], hebb')), instead of
+                          B independent per-slot traces ('slots', the default)
+  batch_norm=True         BatchNorm2d per slot (the reference's batch size 1), running statistics
+                          updated slot by slot; bilinear_upsample=True: align_corners bilinear 2x
   precision='bf16'        config C3: bf16 activations / packed weights on bf16 MFMA with fp32
                           accumulation; parameters, gradients, Adam, logits and the plastic head
                           stay fp32 (base_ch must be a multiple of 32).
@@ -89,8 +94,11 @@ def _check_gpu_tensor(t, what):
 
 class UNetp(nn.Module):
     def __init__(self, n_channels, n_classes, device, alfa_type='free', rule='hebb', nbf=128, batch_norm=False,
-                 bilinear_upsample=False, depth=5, base_ch=8, precision='fp32'):
+                 bilinear_upsample=False, depth=5, base_ch=8, precision='fp32', hebb_mode='slots'):
         super().__init__()
+        if hebb_mode not in ("slots", "sequential"):
+            raise ValueError("hebb_mode must be 'slots' or 'sequential'")
+        self.hebb_mode = hebb_mode
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
         if precision == "bf16" and base_ch % 32:
@@ -130,8 +138,11 @@ class UNetp(nn.Module):
 
     def forward(self, x, hebb):
         single = hebb.dim() == 2
-        if single and x.shape[0] != 1:
+        seq = self.hebb_mode == "sequential"
+        if single and x.shape[0] != 1 and not seq:
             raise ValueError("Only batch size: 1 is supported, but was: %d" % x.shape[0])
+        if seq and not single:
+            raise ValueError("hebb_mode='sequential' threads one [nbf,nbf] trace through the batch")
         if self.alfa_type not in ("free", "yoked"):
             raise ValueError("Must select one plasticity coefficient type ('free' or 'yoked')")
         if self.rule not in ("hebb", "oja"):
@@ -150,7 +161,7 @@ class UNetp(nn.Module):
         if Hh % (1 << (self.depth - 1)):
             raise NotImplementedError("image side %d must be divisible by 2^(depth-1)=%d" % (Hh, 1 << (self.depth - 1)))
         H = hebb.unsqueeze(0) if single else hebb
-        if H.shape != (B, self.nbf, self.nbf):
+        if H.shape != (B if not seq else 1, self.nbf, self.nbf):
             raise ValueError("hebb must be [nbf,nbf] or [B,nbf,nbf]; got %s for batch %d" % (tuple(hebb.shape), B))
         if x.dtype != torch.float32:
             x = x.float()
@@ -163,6 +174,10 @@ class UNetp(nn.Module):
         save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         logits = TrunkFunction.apply(trunk, save, x, *params)
         sink = None if trunk.gradbuf is None else (trunk.gradbuf, self.w, self.alpha)
+        if seq:
+            from punet.head import SequentialHeadFunction
+            Y, Hn = SequentialHeadFunction.apply(logits, hebb, self.w, self.alpha, self.eta, RULES[self.rule], sink)
+            return (Y[0], Hn) if B == 1 else (Y, Hn)
         Y, Hn = PlasticHeadFunction.apply(logits, H, self.w, self.alpha, self.eta, RULES[self.rule], True, sink)
         if single:
             return Y[0], Hn[0]

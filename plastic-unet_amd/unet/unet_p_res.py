@@ -71,8 +71,11 @@ class up(nn.Module):  # unet_p_res.py:200-220
 
 class UNetpRes(nn.Module):
     def __init__(self, n_channels, n_classes, device, neurons=16, dropout_ratio=0.5, alfa_type='free', rule='hebb',
-                 nbf=128, batch_norm=False, bilinear_upsample=False):
+                 nbf=128, batch_norm=False, bilinear_upsample=False, hebb_mode='slots'):
         super().__init__()
+        if hebb_mode not in ("slots", "sequential"):
+            raise ValueError("hebb_mode must be 'slots' or 'sequential'")
+        self.hebb_mode = hebb_mode
         self.n_classes = n_classes
         self.n_channels = n_channels
         self.nbf = nbf
@@ -112,7 +115,10 @@ class UNetpRes(nn.Module):
         from .unet_p import _check_gpu_tensor
         single = hebb.dim() == 2
         B, C, Hh, Ww = x.shape
-        if single and B != 1:
+        seq = self.hebb_mode == "sequential"
+        if seq and not single:
+            raise ValueError("hebb_mode='sequential' threads one [nbf,nbf] trace through the batch")
+        if single and B != 1 and not seq:
             # the reference has no explicit check: activin = x.view(nbf, nbf) fails (S8)
             raise RuntimeError("shape '[%d, %d]' is invalid for input of size %d"
                                % (self.nbf, self.nbf, B * Hh * Ww * self.n_classes))
@@ -131,7 +137,7 @@ class UNetpRes(nn.Module):
         if Hh < 16:
             raise RuntimeError("UNetpRes needs images of at least 16x16 (four 2x2 poolings)")
         H = hebb.unsqueeze(0) if single else hebb
-        if H.shape != (B, self.nbf, self.nbf):
+        if H.shape != (B if not seq else 1, self.nbf, self.nbf):
             raise ValueError("hebb must be [nbf,nbf] or [B,nbf,nbf]; got %s for batch %d" % (tuple(hebb.shape), B))
         if x.dtype != torch.float32:
             x = x.float()
@@ -142,6 +148,10 @@ class UNetpRes(nn.Module):
         save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         logits = ResTrunkFunction.apply(trunk, save, self.training, x, *params)
         sink = None if trunk.gradbuf is None else (trunk.gradbuf, self.w, self.alpha)
+        if seq:
+            from punet.head import SequentialHeadFunction
+            Y, Hn = SequentialHeadFunction.apply(logits, hebb, self.w, self.alpha, self.eta, RULES[self.rule], sink)
+            return (Y[0], Hn) if B == 1 else (Y, Hn)
         Y, Hn = PlasticHeadFunction.apply(logits, H, self.w, self.alpha, self.eta, RULES[self.rule], True, sink)
         if single:
             return Y[0], Hn[0]

@@ -185,3 +185,39 @@ def test_unetp_bn_batched_slots_match_oracle():
         if k == "eta":
             continue
         check_param_grad(k, p.grad, rp[k].grad, True, rp[k.replace(".bias", ".weight")].grad)
+
+
+@pytest.mark.parametrize("rule", ["hebb", "oja"])
+def test_sequential_hebb_mode_matches_oracle(rule):
+    """hebb_mode='sequential': one trace threaded through the batch in order (B successive
+    reference calls sharing the parameters) - outputs, final trace, gradients vs the oracle."""
+    torch.manual_seed(2)
+    ref = oracle.RefUNetp(1, 1, rule=rule, nbf=32, depth=4, base_ch=16)
+    ref.hebb_mode = "sequential"
+    net = UNetp(1, 1, DEV, rule=rule, nbf=32, depth=4, base_ch=16, hebb_mode="sequential")
+    net.load_state_dict(ref.state_dict())
+    g = torch.Generator().manual_seed(8)
+    B = 4
+    x = torch.rand(B, 1, 32, 32, generator=g)
+    t = (torch.rand(B, 32, 32, generator=g) > 0.5).float()
+    H = 0.2 * torch.randn(32, 32, generator=g)
+    yr, hr = ref(x, H)
+    oracle.bce_loss(yr, t).backward()
+    y, h = net(x.to(DEV), H.to(DEV))
+    bce_loss(y, t.to(DEV)).backward()
+    assert y.shape == (B, 32, 32) and h.shape == (32, 32)
+    assert_close(y, yr)
+    assert_close(h, hr)
+    rp = dict(ref.named_parameters())
+    for k, p in net.named_parameters():
+        if k == "eta":
+            assert p.grad is None
+            continue
+        assert_close(p.grad, rp[k].grad, rtol=1e-3, atol_rel=1e-4)
+    # B = 1: identical to the reference call (and to the default 'slots' mode)
+    net2 = UNetp(1, 1, DEV, rule=rule, nbf=32, depth=4, base_ch=16)
+    net2.load_state_dict(ref.state_dict())
+    with torch.no_grad():
+        y1, h1 = net(x[:1].to(DEV), H.to(DEV))
+        y2, h2 = net2(x[:1].to(DEV), H.to(DEV))
+    assert torch.equal(y1, y2) and torch.equal(h1, h2)
