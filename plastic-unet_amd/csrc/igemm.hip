@@ -1023,6 +1023,40 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
     *ksplit = ceil_div(T, *t_per);
 }
 
+// Tile / split plan of one call.  The 6-product kernel does 6x the MFMA work per K stage of the
+// fp32 one for the same loads, so its per-stage fixed cost matters less and its per-block
+// setup/epilogue more: small pixel grids (the 8x8 / 16x16 levels) take the large tiles and split
+// K until ~2 blocks per CU, instead of shrinking the tile to 64x64 (6 MFMAs per wave per stage).
+#ifndef PU_X6_TILES
+#define PU_X6_TILES 1
+#endif
+static bool uses_x6(const pu_conv_args* a);
+static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
+    if (!(PU_X6_TILES && uses_x6(a))) {
+        choose_tile(M, a->n, bm, bn);
+        plan_split(a, M, *bm, *bn, ksplit, t_per);
+        return;
+    }
+    const int N = a->n;
+    const int T = a->k_pad / IG_BK;
+    if (N <= 64) {
+        *bn = 64;
+        *bm = blocks_for(M, N, 256, 64) >= 480 ? 256 : 128;
+    } else {
+        *bn = 128;
+        *bm = 128;
+    }
+    *ksplit = 1;
+    *t_per = T;
+    const int tiles = blocks_for(M, N, *bm, *bn);
+    if (tiles >= 480 || !vec_epilogue(a)) return;
+    int ks = ceil_div(512, tiles);
+    if (ks > T / 8) ks = T / 8;
+    if (ks < 2) return;
+    *t_per = ceil_div(T, ks);
+    *ksplit = ceil_div(T, *t_per);
+}
+
 // the small-channel direct convolution handles: 3x3 / s1 / p1 (same size), C in {1,4,8,12,16},
 // N in {4,8,16}, tap-major weight rows, float4 epilogue
 #ifndef PU_NO_SMALLCONV
@@ -1036,6 +1070,10 @@ static bool small_conv_ok(const pu_conv_args* a) {
     return !PU_NO_SMALLCONV && cset && nset && nc && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
            a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) && vec_epilogue(a) &&
            (a->cgroup == 0 || a->cgroup >= C) && (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
+}
+
+static bool uses_x6(const pu_conv_args* a) {
+    return a->weight6 && choose_mode(a->c0, a->c1) == LOAD_CHUNK16 && !PU_NO_DMA && !small_conv_ok(a);
 }
 
 static size_t split_bytes(long long M, int n, int ksplit) {
@@ -1114,9 +1152,8 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         return check_launch("pu_conv_igemm (small-channel)");
     }
     int bm, bn;
-    choose_tile(M, N, &bm, &bn);
+    plan_tiles(a, M, &bm, &bn, &p.ksplit, &p.t_per);
     p.gn = ceil_div(N, bn);
-    plan_split(a, M, bm, bn, &p.ksplit, &p.t_per);
     if (p.ksplit > 1 && (!a->workspace || a->ws_bytes < split_bytes(M, N, p.ksplit))) {
         p.ksplit = 1;                       // no scratch: unsplit
         p.t_per = a->k_pad / IG_BK;
@@ -1163,17 +1200,17 @@ extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
     const long long M = (long long)a->batch * a->out_h * a->out_w;
     if (small_conv_ok(a)) return 0;
     int bm, bn, ks, tp;
-    choose_tile(M, a->n, &bm, &bn);
-    plan_split(a, M, bm, bn, &ks, &tp);
+    plan_tiles(a, M, &bm, &bn, &ks, &tp);
     return split_bytes(M, a->n, ks);
 }
 
 extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* mode, int* ksplit) {
     PU_REQUIRE(a && bm && bn && mode, "pu_conv_igemm_tile: null args");
     const long long M = (long long)a->batch * a->out_h * a->out_w;
-    choose_tile(M, a->n, bm, bn);
+    int ks, tp;
+    plan_tiles(a, M, bm, bn, &ks, &tp);
     *mode = choose_mode(a->c0, a->c1);
-    if (a->weight6 && *mode == LOAD_CHUNK16 && !PU_NO_DMA && !small_conv_ok(a)) *mode = 4;   // 6-product bf16
+    if (uses_x6(a)) *mode = 4;   // 6-product bf16
     if (small_conv_ok(a)) {          // reported as mode 3 ("direct"), tile SC_TH x SC_TW pixels
         *bm = SC_TH * SC_TW;
         *bn = a->n;
@@ -1181,10 +1218,6 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         if (ksplit) *ksplit = 1;
         return PU_OK;
     }
-    if (ksplit) {
-        int ks, tp;
-        plan_split(a, M, *bm, *bn, &ks, &tp);
-        *ksplit = (ks > 1 && a->workspace && a->ws_bytes >= split_bytes(M, a->n, ks)) ? ks : 1;
-    }
+    if (ksplit) *ksplit = (ks > 1 && a->workspace && a->ws_bytes >= split_bytes(M, a->n, ks)) ? ks : 1;
     return PU_OK;
 }
