@@ -576,15 +576,29 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
 // co-issues with the MFMAs).  Same loader, ring, swizzle, epilogue and split-K as the fp32 kernel.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
+#ifndef PU_X6_SCALAR_SUB
+#define PU_X6_SCALAR_SUB 0   // 1: residual subtractions as scalar v_sub_f32 (no SLP-packed v_pk_add_f32)
+#endif
+
+__device__ __forceinline__ float x6_sub(float a, float b) {
+#if PU_X6_SCALAR_SUB
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return a - b;
+#endif
+}
+
 __device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf16x8_t& h, bf16x8_t& m, bf16x8_t& l) {
 #pragma clang fp contract(off)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const float x = e < 4 ? lo4[e] : hi4[e - 4];
         const __bf16 a = (__bf16)x;
-        const float r = x - (float)a;
+        const float r = x6_sub(x, (float)a);
         const __bf16 b = (__bf16)r;
-        const float q = r - (float)b;
+        const float q = x6_sub(r, (float)b);
         h[e] = a;
         m[e] = b;
         l[e] = (__bf16)q;
@@ -605,6 +619,13 @@ __device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf
 #endif
 #ifndef PU_X6_IL
 #define PU_X6_IL 0       // sched_group_barrier: interleave each MFMA with VALU/SALU work
+#endif
+#ifndef PU_X6_W41
+#define PU_X6_W41 1      // 128x128 tile as 4 waves along M (each 32 pixels x 128 channels): one pixel
+                         // split feeds 4 weight fragments (24 MFMAs), 2x2 waves split twice as much
+#endif
+#ifndef PU_X6_ORDER
+#define PU_X6_ORDER 0    // 0: per pixel fragment split + 6 FN MFMAs; 1: all splits first, term-major MFMAs
 #endif
 
 template <int BM, int BN, int WM, int WN, int NBUF, int KSUB>
@@ -756,6 +777,24 @@ __global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
                 for (int j = 0; j < FN; ++j)
                     fw[pl][j] = *reinterpret_cast<const bf16x8_t*>(wp + ((pl * 2 + lh) * BN + b_row0 + j * 32) * 4);
             if (PU_X6_SCHED == 0 && u == 0) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
+            if (PU_X6_ORDER == 1) {
+                bf16x8_t xs3[3][FM];
+#pragma unroll
+                for (int i = 0; i < FM; ++i) split3_bf16(xa[i], xb[i], xs3[0][i], xs3[1][i], xs3[2][i]);
+                // terms (w plane, x plane), small first; independent accumulators rotate
+                constexpr int TW[6] = {1, 2, 0, 1, 0, 0};
+                constexpr int TX[6] = {1, 0, 2, 0, 1, 0};
+#pragma unroll
+                for (int tt = 0; tt < 6; ++tt) {
+#pragma unroll
+                    for (int i = 0; i < FM; ++i)
+#pragma unroll
+                        for (int j = 0; j < FN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[TW[tt]][j], xs3[TX[tt]][i], acc[i][j], 0, 0, 0);
+                    if (PU_X6_SCHED == 1 && u == 0 && tt == 1) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
+                }
+                continue;
+            }
 #pragma unroll
             for (int i = 0; i < FM; ++i) {
                 bf16x8_t xh, xm, xl;
@@ -1165,7 +1204,10 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         PU_REQUIRE(((uintptr_t)a->weight6 & 15) == 0, "pu_conv_igemm: weight6 must be 16-byte aligned");
 #define PU_X6(BM_, BN_, WM_, WN_) hipLaunchKernelGGL((igemm_x6_kernel<BM_, BN_, WM_, WN_, PU_X6_NBUF, PU_X6_KSUB>), grid, dim3(256), 0, s, p)
         if (bm == 256) PU_X6(256, 64, 4, 1);
-        else if (bm == 128 && bn == 128) PU_X6(128, 128, 2, 2);
+        else if (bm == 128 && bn == 128) {
+            if (PU_X6_W41) PU_X6(128, 128, 4, 1);
+            else PU_X6(128, 128, 2, 2);
+        }
         else if (bm == 128) PU_X6(128, 64, 2, 2);
         else PU_X6(64, 64, 2, 2);
 #undef PU_X6

@@ -679,6 +679,9 @@ static bool small_wgrad_ok(const pu_wgrad_args* a) {
            (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
 }
 
+#ifndef PU_WG_X6_BK256
+#define PU_WG_X6_BK256 1
+#endif
 static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     PU_REQUIRE(a && a->batch > 0 && a->out_h > 0 && a->out_w > 0 && a->in_h > 0 && a->in_w > 0, "pu_wgrad: bad grid");
     PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0, "pu_wgrad: bad taps");
@@ -733,6 +736,13 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
         pl->BN = 64; pl->BK = b192 ? 192 : 128; occ = b192 ? 3 : 4;
     }
     else { pl->BN = 128; pl->BK = 128; occ = pl->dma ? 3 : 4; }
+    // 6-product path: a 128 x 256 tile (2x2 waves of 64 x 128) splits 6 operand fragments per 48
+    // MFMAs instead of 4 per 24, when K pads no worse than with 128 (PU_WG_X6_BK256 knob)
+    if (PU_WG_X6_BK256 && a->math == 1 && pl->dma && pl->BN == 128 &&
+        ceil_div(ext_k, 256) * 256 <= ceil_div(ext_k, 128) * 128) {
+        pl->BK = 256;
+        occ = 2;
+    }
     pl->gx = ceil_div(ext_k, pl->BK);
     pl->gy = ceil_div(ext_n, pl->BN);
     const int tiles = pl->gx * pl->gy;
@@ -1104,6 +1114,7 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
             if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
             else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
             else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
+            else if (pl.BK == 256) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true>), grid, dim3(256), 0, s, p);
             else PU_WG_DMA(128, 128, 2, 2);
         } else if (pl.qvec) {
             if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, true);
