@@ -628,20 +628,20 @@ __device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf
 #define PU_X6_ORDER 0    // 0: per pixel fragment split + 6 FN MFMAs; 1: all splits first, term-major MFMAs
 #endif
 
-template <int BM, int BN, int WM, int WN, int NBUF, int KSUB>
-__global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
+template <int BM, int BN, int WM, int WN, int NBUF, int KSUB, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) {
     constexpr int FM = BM / WM / 32;
     constexpr int FN = BN / WN / 32;
-    constexpr int A_LD = BM / 64;             // pixel rows: glds per wave per sub-stage (16 rows x 64 B)
+    constexpr int A_LD = BM / (16 * NW);      // pixel rows: glds per wave per sub-stage (16 rows x 64 B)
     constexpr int W_TOT = 6 * BN / 64;        // weight planes: glds per block per sub-stage (64 x 16 B)
-    constexpr int W_LD = (W_TOT + 3) / 4;     // per wave (surplus ones load the zero page into a sink)
-    constexpr bool SINK = (W_TOT % 4) != 0;
+    constexpr int W_LD = (W_TOT + NW - 1) / NW;   // per wave (surplus ones load the zero page into a sink)
+    constexpr bool SINK = (W_TOT % NW) != 0;
     constexpr int G = (A_LD + W_LD) * KSUB;   // loads per wave per ring slot
     constexpr int A_FL = BM * 16;             // floats of one sub-stage's pixel image
     constexpr int W_FL = BN * 6 * 4;          // float-sized slots of one sub-stage's weight planes
     constexpr int SUB = A_FL + W_FL;
     constexpr int STAGE = KSUB * SUB;
-    static_assert(WM * WN == 4, "4 waves");
+    static_assert(WM * WN == NW && A_LD >= 1, "wave grid");
 
     __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE + (SINK ? 256 : 0)];
 
@@ -663,7 +663,7 @@ __global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
     unsigned tmask[A_LD];
 #pragma unroll
     for (int j = 0; j < A_LD; ++j) {
-        const int m = m_blk + wave * (BM / 4) + 16 * j + lq;
+        const int m = m_blk + wave * (BM / NW) + 16 * j + lq;
         rb0[j] = 0; rb1[j] = 0; tmask[j] = 0;
         if (m < p.M) {
             const int t = fdiv(m, p.dWo);
@@ -688,7 +688,7 @@ __global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
     const __bf16* wrow[W_LD];
 #pragma unroll
     for (int j = 0; j < W_LD; ++j) {
-        const int I = wave + 4 * j;
+        const int I = wave + NW * j;
         const int e = I * 64 + lane;
         const int q = e / BN, row = e - q * BN;
         const int n = n_blk + row;
@@ -721,12 +721,12 @@ __global__ __launch_bounds__(256) void igemm_x6_kernel(const IgemmParams p) {
 #pragma unroll
         for (int j = 0; j < A_LD; ++j) {
             const float* g = (tmask[j] & bit) ? src + (first ? rb0[j] : rb1[j]) + off : g_zero16;
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(a_slot + (wave * (BM / 4) + 16 * j) * 16),
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(a_slot + (wave * (BM / NW) + 16 * j) * 16),
                                              16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < W_LD; ++j) {
-            const int I = wave + 4 * j;
+            const int I = wave + NW * j;
             const void* g = (live && wrow[j]) ? (const void*)(wrow[j] + wo) : (const void*)g_zero16;
             float* dst = (!SINK || I < W_TOT) ? w_slot + I * 256 : lds + NBUF * STAGE;   // 64 lanes x 16 B
             __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)dst, 16, 0, 0);
@@ -1069,6 +1069,10 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
 #ifndef PU_X6_TILES
 #define PU_X6_TILES 1
 #endif
+#ifndef PU_X6_BIG
+#define PU_X6_BIG 1      // long-K layers (k_pad >= 2048): 1 = 256x128 8-wave tiles, 2 = also 256x256
+                         // for N >= 256 (measured slower); 0 = 128x128 4-wave tiles everywhere
+#endif
 static bool uses_x6(const pu_conv_args* a);
 static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
     if (!(PU_X6_TILES && uses_x6(a))) {
@@ -1078,9 +1082,17 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
     }
     const int N = a->n;
     const int T = a->k_pad / IG_BK;
+    int target = 512;                 // ~2 resident blocks per CU (4-wave tiles)
     if (N <= 64) {
         *bn = 64;
         *bm = blocks_for(M, N, 256, 64) >= 480 ? 256 : 128;
+    } else if (PU_X6_BIG && a->k_pad >= 2048) {
+        // 8 waves, one block per CU (85 KB of LDS), each wave 32 pixels x 128 channels: fewer
+        // LDS-DMA pieces and global bytes per MFMA than two 128 x 128 blocks; +2-4% on the
+        // long-K layers (16x16 / 32x32 levels), a loss on short-K ones (K = 576: l2_cat dgrad)
+        *bn = (N >= 256 && PU_X6_BIG > 1) ? 256 : 128;
+        *bm = 256;
+        target = 256;
     } else {
         *bn = 128;
         *bm = 128;
@@ -1088,8 +1100,8 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
     *ksplit = 1;
     *t_per = T;
     const int tiles = blocks_for(M, N, *bm, *bn);
-    if (tiles >= 480 || !vec_epilogue(a)) return;
-    int ks = ceil_div(512, tiles);
+    if (tiles >= target - target / 16 || !vec_epilogue(a)) return;
+    int ks = ceil_div(target, tiles);
     if (ks > T / 8) ks = T / 8;
     if (ks < 2) return;
     *t_per = ceil_div(T, ks);
@@ -1203,7 +1215,11 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         p.wt = reinterpret_cast<const float*>(a->weight6);
         PU_REQUIRE(((uintptr_t)a->weight6 & 15) == 0, "pu_conv_igemm: weight6 must be 16-byte aligned");
 #define PU_X6(BM_, BN_, WM_, WN_) hipLaunchKernelGGL((igemm_x6_kernel<BM_, BN_, WM_, WN_, PU_X6_NBUF, PU_X6_KSUB>), grid, dim3(256), 0, s, p)
-        if (bm == 256) PU_X6(256, 64, 4, 1);
+        if (bm == 256 && bn == 256)
+            hipLaunchKernelGGL((igemm_x6_kernel<256, 256, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
+        else if (bm == 256 && bn == 128)
+            hipLaunchKernelGGL((igemm_x6_kernel<256, 128, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
+        else if (bm == 256) PU_X6(256, 64, 4, 1);
         else if (bm == 128 && bn == 128) {
             if (PU_X6_W41) PU_X6(128, 128, 4, 1);
             else PU_X6(128, 128, 2, 2);

@@ -638,9 +638,17 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
         const int n = int(idx / Kc);
         const int k = int(idx - (long long)n * Kc);
         if (n >= N) return;
-        double s = 0.0;
-        for (int g = 0; g < G; ++g) s += (double)part[(long long)g * total + idx];
-        const float v = (float)s;
+        // 4 independent fp64 chains (fixed interleave, deterministic): keeps 4 loads in flight
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int g = 0;
+        for (; g + 3 < G; g += 4) {
+            s0 += (double)part[(long long)g * total + idx];
+            s1 += (double)part[(long long)(g + 1) * total + idx];
+            s2 += (double)part[(long long)(g + 2) * total + idx];
+            s3 += (double)part[(long long)(g + 3) * total + idx];
+        }
+        for (; g < G; ++g) s0 += (double)part[(long long)g * total + idx];
+        const float v = (float)((s0 + s1) + (s2 + s3));
         if (k < K) {
             const int tap = k / C, c = k - tap * C;
             const int r = tap / kw, ss = tap - r * kw;
