@@ -253,6 +253,7 @@ def main():
         mfma = {t: d for t, d in summ.items() if d["flops"] and (t.startswith("igemm") or t.startswith("wgrad"))}
         dom = max(mfma.items(), key=lambda kv: kv[1]["ms"])
         dtag, dd = dom
+        hbm_bound = "direct" in dtag and dd["bytes"] > 0   # small-channel direct convs (C4/C5 levels)
         if args.config == "c3":     # v_mfma_f32_32x32x16_bf16: 4096 FLOP/clk/CU dense
             peak = f32peak * 16.0
             basis = "bf16 MFMA 4096 FLOP/clk/CU x %d CU x %.2f GHz (dense)" % (cu, clk)
@@ -275,6 +276,13 @@ def main():
                                   "frac": round(tot_f / (tot_ms * 1e-3) / 1e12 / peak, 4),
                                   "flop_per_step": tot_f / nprof, "ms_per_step": round(tot_ms / nprof, 3)},
                 "peak_basis": basis}
+        if hbm_bound:   # HBM roofline: algorithmic bytes per launch / launch time vs 8 TB/s
+            gbs = dd["bytes"] / (dd["ms"] * 1e-3) / 1e9
+            roof.update({"bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
+                         "frac": round(gbs / 8000.0, 4), "algorithmic_bytes_per_launch": dd["bytes"] / dd["launches"],
+                         "mfma_tflop_s": round(ach, 2),
+                         "peak_basis": "HBM3E 8 TB/s (MI355X_MICROARCH.md); direct small-channel conv, "
+                                       "algorithmic bytes = inputs + outputs + masks"})
         prof_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof_path):
             try:
