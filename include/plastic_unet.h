@@ -169,17 +169,21 @@ int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t workspace_byt
  *   batch size 1) and the running statistics take the B per-slot updates in slot order
  *   (running = (1-m) running + m stat, unbiased variance; NULL running buffers: no update);
  *   save_mean / save_rstd [batch][c].  eval (training = 0): running statistics, save_* [c].
- *   y = relu?((z - mean) * rstd * gamma + beta); gamma / beta may be NULL (affine=False).
- * pu_bn_bwd: given g = dL/dy (ReLU mask applied), dz and dgamma / dbeta [c] (NULL: skipped).
+ *   y = relu?((z - mean) * rstd * gamma + beta [+ resid]); gamma / beta may be NULL
+ *   (affine=False); resid (optional, NHWC like z): the residual_block add before the ReLU
+ *   (unet_p_res.py:188).
+ * pu_bn_bwd: given g = dL/dy (ReLU mask applied), dz = (BN backward [+ add]) * (mask > 0) with
+ *   add / mask optional, and dgamma / dbeta [c] (NULL: skipped).
  * fp64 partial sums, fixed-order reduction (deterministic).  c % 4 == 0, NHWC, 16-B aligned.
  * ------------------------------------------------------------------------------------------- */
 size_t pu_bn_workspace_bytes(int batch, long long hw, int c);
 int pu_bn_fwd(const float* z, const float* gamma, const float* beta, float* running_mean, float* running_var,
               float* y, float* save_mean, float* save_rstd, int batch, long long hw, int c, float eps,
-              float momentum, int training, int relu, void* workspace, size_t workspace_bytes, void* stream);
+              float momentum, int training, int relu, const float* resid, void* workspace,
+              size_t workspace_bytes, void* stream);
 int pu_bn_bwd(const float* z, const float* g, const float* save_mean, const float* save_rstd,
               const float* gamma, float* dz, float* dgamma, float* dbeta, int batch, long long hw, int c,
-              void* workspace, size_t workspace_bytes, void* stream);
+              const float* add, const float* mask, void* workspace, size_t workspace_bytes, void* stream);
 
 /* nn.Upsample(scale_factor=2, mode='bilinear', align_corners=True) of up(bilinear=True)
  * src/unet/unet_p.py:235-236, NHWC x [batch][h][w][c] -> y [batch][2h][2w][c]; the backward

@@ -360,6 +360,12 @@ class RefUNetpRes(_PlasticBase):
         self.outc = _Outconv(n, n_classes)
 
     def trunk(self, x):
+        # batch_norm=True: per-slot BatchNorm statistics in training mode (see RefUNetp.trunk)
+        if self.training and x.shape[0] > 1 and any(isinstance(m, nn.BatchNorm2d) for m in self.modules()):
+            return torch.cat([self._trunk(x[b:b + 1]) for b in range(x.shape[0])])
+        return self._trunk(x)
+
+    def _trunk(self, x):
         xc1 = self.conv1(x)
         xc2 = self.conv2(self.pool1(xc1))
         xc3 = self.conv3(self.pool2(xc2))

@@ -107,8 +107,9 @@ __global__ void bn_stats_finalize_kernel(const double* __restrict__ part, int S,
 // (stat_stride = C) or per channel (eval: stat_stride = 0, from the running statistics)
 __global__ void bn_apply_kernel(const float* __restrict__ z, const float* __restrict__ mean,
                                 const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                const float* __restrict__ beta, float* __restrict__ y, long long hw, int C,
-                                int stat_stride, long long total4, int relu) {
+                                const float* __restrict__ beta, const float* __restrict__ resid,
+                                float* __restrict__ y, long long hw, int C, int stat_stride, long long total4,
+                                int relu) {
 #pragma clang fp contract(off)
     const int C4 = C >> 2;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total4;
@@ -118,11 +119,13 @@ __global__ void bn_apply_kernel(const float* __restrict__ z, const float* __rest
         const float* mu = mean + b * stat_stride + c;
         const float* rs = rstd + b * stat_stride + c;
         f32x4 v = reinterpret_cast<const f32x4*>(z)[i];
+        const f32x4 rv = resid ? reinterpret_cast<const f32x4*>(resid)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const float a = rs[e] * (gamma ? gamma[c + e] : 1.f);
             const float bb = (beta ? beta[c + e] : 0.f) - mu[e] * a;
             float o = v[e] * a + bb;
+            if (resid) o = o + rv[e];         // residual_block: BN output + relu(input) (unet_p_res.py:188)
             if (relu) o = fmaxf(o, 0.f);
             v[e] = o;
         }
@@ -169,6 +172,7 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int S, i
 __global__ void bn_bwd_apply_kernel(const float* __restrict__ z, const float* __restrict__ g,
                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                     const float* __restrict__ coef, const float* __restrict__ gamma,
+                                    const float* __restrict__ add, const float* __restrict__ mask,
                                     float* __restrict__ dz, long long hw, int C, long long total4) {
 #pragma clang fp contract(off)
     const int C4 = C >> 2;
@@ -185,6 +189,16 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ z, const float* __
             const float gm = coef[bc * 2], k = coef[bc * 2 + 1];
             const float xm = (zv[e] - mean[bc]) * k;
             o[e] = (gv[e] - gm - xm) * rstd[bc] * (gamma ? gamma[c + e] : 1.f);
+        }
+        if (add) {
+            const f32x4 av = reinterpret_cast<const f32x4*>(add)[i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = o[e] + av[e];
+        }
+        if (mask) {
+            const f32x4 mv = reinterpret_cast<const f32x4*>(mask)[i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) o[e] = 0.f;
         }
         reinterpret_cast<f32x4*>(dz)[i] = o;
     }
@@ -318,10 +332,11 @@ extern "C" size_t pu_bn_workspace_bytes(int batch, long long hw, int c) {
 
 extern "C" int pu_bn_fwd(const float* z, const float* gamma, const float* beta, float* running_mean,
                          float* running_var, float* y, float* save_mean, float* save_rstd, int batch, long long hw,
-                         int c, float eps, float momentum, int training, int relu, void* workspace, size_t ws_bytes,
-                         void* stream) {
+                         int c, float eps, float momentum, int training, int relu, const float* resid,
+                         void* workspace, size_t ws_bytes, void* stream) {
     PU_REQUIRE(z && y && save_mean && save_rstd && batch > 0 && hw > 0 && c > 0, "pu_bn_fwd: bad args");
-    PU_REQUIRE(c % 4 == 0 && (((uintptr_t)z | (uintptr_t)y) & 15) == 0, "pu_bn_fwd: channels %% 4, 16-byte alignment");
+    PU_REQUIRE(c % 4 == 0 && (((uintptr_t)z | (uintptr_t)y | (uintptr_t)resid) & 15) == 0,
+               "pu_bn_fwd: channels %% 4, 16-byte alignment");
     PU_REQUIRE((running_mean == nullptr) == (running_var == nullptr), "pu_bn_fwd: running buffers go together");
     hipStream_t s = as_stream(stream);
     const long long total4 = (long long)batch * hw * c / 4;
@@ -329,8 +344,8 @@ extern "C" int pu_bn_fwd(const float* z, const float* gamma, const float* beta, 
         PU_REQUIRE(running_mean, "pu_bn_fwd: eval mode needs the running statistics");
         hipLaunchKernelGGL(bn_eval_stats_kernel, dim3((c + 255) / 256), dim3(256), 0, s, running_mean, running_var, eps, c,
                            save_mean, save_rstd);
-        hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(total4)), dim3(256), 0, s, z, save_mean, save_rstd, gamma, beta, y,
-                           hw, c, 0, total4, relu);
+        hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(total4)), dim3(256), 0, s, z, save_mean, save_rstd, gamma, beta,
+                           resid, y, hw, c, 0, total4, relu);
         return check_launch("pu_bn_fwd (eval)");
     }
     const BnPlan pl = bn_plan(batch, hw, c);
@@ -341,16 +356,16 @@ extern "C" int pu_bn_fwd(const float* z, const float* gamma, const float* beta, 
                        nullptr, batch, hw, c, pl.CC, pl.S, part);
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((c + 255) / 256), dim3(256), 0, s, part, pl.S, batch, c, hw, eps,
                        momentum, save_mean, save_rstd, running_mean, running_var);
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(total4)), dim3(256), 0, s, z, save_mean, save_rstd, gamma, beta, y,
-                       hw, c, c, total4, relu);
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(ew_grid(total4)), dim3(256), 0, s, z, save_mean, save_rstd, gamma, beta,
+                       resid, y, hw, c, c, total4, relu);
     return check_launch("pu_bn_fwd");
 }
 
 extern "C" int pu_bn_bwd(const float* z, const float* g, const float* save_mean, const float* save_rstd,
                          const float* gamma, float* dz, float* dgamma, float* dbeta, int batch, long long hw, int c,
-                         void* workspace, size_t ws_bytes, void* stream) {
+                         const float* add, const float* mask, void* workspace, size_t ws_bytes, void* stream) {
     PU_REQUIRE(z && g && save_mean && save_rstd && dz && batch > 0 && hw > 0 && c > 0, "pu_bn_bwd: bad args");
-    PU_REQUIRE(c % 4 == 0 && (((uintptr_t)z | (uintptr_t)g | (uintptr_t)dz) & 15) == 0,
+    PU_REQUIRE(c % 4 == 0 && (((uintptr_t)z | (uintptr_t)g | (uintptr_t)dz | (uintptr_t)add | (uintptr_t)mask) & 15) == 0,
                "pu_bn_bwd: channels %% 4, 16-byte alignment");
     if (!workspace || ws_bytes < pu_bn_workspace_bytes(batch, hw, c))
         return fail(PU_ERR_WORKSPACE, "pu_bn_bwd: workspace %zu < %zu", ws_bytes, pu_bn_workspace_bytes(batch, hw, c));
@@ -364,7 +379,7 @@ extern "C" int pu_bn_bwd(const float* z, const float* g, const float* save_mean,
                        coef, dgamma, dbeta);
     const long long total4 = (long long)batch * hw * c / 4;
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid(total4)), dim3(256), 0, s, z, g, save_mean, save_rstd, coef,
-                       gamma, dz, hw, c, total4);
+                       gamma, add, mask, dz, hw, c, total4);
     return check_launch("pu_bn_bwd");
 }
 

@@ -103,8 +103,8 @@ SIGNATURES = [
     ("pu_bce_fwd", c_int, [P, P, c_ll, P, P, c_size, P]),
     ("pu_bce_bwd", c_int, [P, P, c_ll, P, P, P]),
     ("pu_bn_workspace_bytes", c_size, [c_int, c_ll, c_int]),
-    ("pu_bn_fwd", c_int, [P, P, P, P, P, P, P, P, c_int, c_ll, c_int, c_float, c_float, c_int, c_int, P, c_size, P]),
-    ("pu_bn_bwd", c_int, [P, P, P, P, P, P, P, P, c_int, c_ll, c_int, P, c_size, P]),
+    ("pu_bn_fwd", c_int, [P, P, P, P, P, P, P, P, c_int, c_ll, c_int, c_float, c_float, c_int, c_int, P, P, c_size, P]),
+    ("pu_bn_bwd", c_int, [P, P, P, P, P, P, P, P, c_int, c_ll, c_int, P, P, P, c_size, P]),
     ("pu_upsample_bilinear2x_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_upsample_bilinear2x_bwd", c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_adam_multi", c_int, [ctypes.POINTER(AdamTensor), c_int, c_float, c_float, c_float, c_float, c_float,

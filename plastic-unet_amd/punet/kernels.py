@@ -472,11 +472,11 @@ def adam_multi(params, grads, exp_avgs, exp_avg_sqs, beta1, beta2, eps, weight_d
 
 
 # --------------------------------------------------------------------- BatchNorm2d / bilinear 2x
-def bn_fwd(z, gamma, beta, running_mean, running_var, eps, momentum, training, relu=True):
+def bn_fwd(z, gamma, beta, running_mean, running_var, eps, momentum, training, relu=True, resid=None):
     """BatchNorm2d (+ReLU) over NHWC z [B,H,W,C].  training: per-slot statistics over H x W (the
     reference's bs=1 BatchNorm, slot by slot) and B in-order running-statistic updates; else the
-    running statistics.  Returns (y, save_mean [B,C] or [C], save_rstd)."""
-    _req(z, "z")
+    running statistics; resid is added before the ReLU.  Returns (y, save_mean [B,C] or [C], save_rstd)."""
+    _req(z, "z"); _req(resid, "resid")
     B, H, W, C = z.shape
     y = torch.empty_like(z)
     shape = (B, C) if training else (C,)
@@ -488,14 +488,15 @@ def bn_fwd(z, gamma, beta, running_mean, running_var, eps, momentum, training, r
     with _Rec("batchnorm_fwd", nbytes=4.0 * (3 if training else 2) * z.numel()):
         check(L.pu_bn_fwd(z.data_ptr(), _p(gamma), _p(beta), _p(running_mean), _p(running_var), y.data_ptr(),
                           mean.data_ptr(), rstd.data_ptr(), B, H * W, C, float(eps), float(momentum),
-                          1 if training else 0, 1 if relu else 0, ws.data_ptr(), nbytes, _stream()), "pu_bn_fwd")
+                          1 if training else 0, 1 if relu else 0, _p(resid), ws.data_ptr(), nbytes, _stream()),
+              "pu_bn_fwd")
     return y, mean, rstd
 
 
-def bn_bwd(z, g, mean, rstd, gamma, dgamma=None, dbeta=None):
+def bn_bwd(z, g, mean, rstd, gamma, dgamma=None, dbeta=None, add=None, mask=None):
     """Backward of the training-mode BatchNorm2d given g = dL/d(BN output) (ReLU mask already
-    applied): returns dz; writes dgamma / dbeta [C] when given."""
-    _req(z, "z"); _req(g, "g")
+    applied): returns dz (+ add, times (mask > 0) when given); writes dgamma / dbeta [C]."""
+    _req(z, "z"); _req(g, "g"); _req(add, "add"); _req(mask, "mask")
     B, H, W, C = z.shape
     dz = torch.empty_like(z)
     L = lib()
@@ -503,7 +504,8 @@ def bn_bwd(z, g, mean, rstd, gamma, dgamma=None, dbeta=None):
     ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=z.device)
     with _Rec("batchnorm_bwd", nbytes=4.0 * 5 * z.numel()):
         check(L.pu_bn_bwd(z.data_ptr(), g.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _p(gamma), dz.data_ptr(),
-                          _p(dgamma), _p(dbeta), B, H * W, C, ws.data_ptr(), nbytes, _stream()), "pu_bn_bwd")
+                          _p(dgamma), _p(dbeta), B, H * W, C, _p(add), _p(mask), ws.data_ptr(), nbytes, _stream()),
+              "pu_bn_bwd")
     return dz
 
 

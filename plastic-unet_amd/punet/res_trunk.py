@@ -155,6 +155,24 @@ class ResTrunk:
             self.params += self._stack_params(mod.uconv[1].mconv)
         self.slots["outc"] = len(self.params)
         self.params += [model.outc.conv.weight, model.outc.conv.bias]
+        # batch_norm=True (unet_p_res.py:171-176): each residual block of the DOWN stacks and mid
+        # carries one BatchNorm2d on its ReLU'd input, before conv A (its conv_modules are built
+        # without batch_norm, :174-175); the up stages' middle has none (:211).  Affine params
+        # appended after outc.
+        self.bn = {}             # (stack, block) -> (param index, module)
+        for name in self.DOWN + ("mid",):
+            mod = getattr(model, name)
+            seq = mod.dconv if name != "mid" else mod.mconv
+            for blk in (1, 2):
+                layers = list(seq[blk].conv)
+                if len(layers) == 3:
+                    continue
+                m = layers[1]
+                if not isinstance(m, torch.nn.BatchNorm2d) or m.momentum is None:
+                    raise NotImplementedError("UNetpRes BatchNorm layout not recognised")
+                self.bn[(name, blk)] = (len(self.params), m)
+                self.params += [m.weight, m.bias]
+        self.training = True
         self.gradbuf = None
         self.mask_fn = None      # (name, batch, channels, p) -> [B, C] scale; default: bernoulli
         self.debug = None
@@ -164,15 +182,17 @@ class ResTrunk:
         out = [seq[0].weight, seq[0].bias]
         for blk in (seq[1], seq[2]):
             layers = list(blk.conv)
-            if len(layers) != 3:
-                raise NotImplementedError("UNetpRes(batch_norm=True) is not built on the MI355X path")
-            for cm in layers[1:]:
-                out += [cm.conv.weight, cm.conv.bias]
+            convs = layers[1:] if len(layers) == 3 else layers[2:]      # [ReLU, (BN,) A, B]
+            for cm in convs:
+                conv = cm.conv if isinstance(cm.conv, torch.nn.Conv2d) else cm.conv[0]
+                out += [conv.weight, conv.bias]
         return out
 
     def backward_order(self):
-        """Parameters in the order backward() completes their gradients (outc first, conv1 last)."""
-        return list(reversed(self.params))
+        """Parameters in the order backward() completes their gradients (outc first, conv1 last;
+        the BatchNorm affine parameters last - they are small)."""
+        n_core = self.slots["outc"] + 2
+        return list(reversed(self.params[:n_core])) + list(reversed(self.params[n_core:]))
 
     def _ready(self, i, n=2):
         """params[i:i+n]'s gradient kernels are enqueued: let an armed BucketReducer know."""
@@ -192,6 +212,33 @@ class ResTrunk:
         return torch.empty(B, C, dtype=torch.float32, device=device).bernoulli_(1.0 - p).div_(1.0 - p)
 
     # ---------------------------------------------------------------------------- forward
+    def _bn(self, P, key, z, relu, resid=None, save=None):
+        j, m = self.bn[key]
+        training = self.training or not m.track_running_stats
+        update = self.training and m.track_running_stats
+        y, mean, rstd = K.bn_fwd(z, P[j], P[j + 1], m.running_mean if (update or not training) else None,
+                                 m.running_var if (update or not training) else None, m.eps, m.momentum, training,
+                                 relu=relu, resid=resid)
+        if update:
+            m.num_batches_tracked.add_(z.shape[0])     # one reference forward per slot
+        return y, (mean, rstd)
+
+    def _stack_fwd_bn(self, P, i, name, x0, x1=None):
+        """conv0 + ReLU, then per residual block: n = BN(r); a = relu(A(n)); r' = relu(B(a) + r)
+        (unet_p_res.py:166-189 with batch_norm=True; the add and ReLU fused in B's epilogue)."""
+        pk = self.packs
+        r = conv3x3(x0, P[i], P[i + 1], pk, x1=x1)
+        st = {"x0": x0, "x1": x1}
+        for blk in (1, 2):
+            ia = i + 2 + 4 * (blk - 1)
+            n, sa = self._bn(P, (name, blk), r, relu=False)
+            a = conv3x3(n, P[ia], P[ia + 1], pk)
+            r_next = conv3x3(a, P[ia + 2], P[ia + 3], pk, resid=r)
+            st[blk] = (r, n, a, sa)
+            r = r_next
+        st["y"] = r
+        return r, st
+
     def _stack_fwd(self, P, i, x0, x1=None):
         pk = self.packs
         r1 = conv3x3(x0, P[i], P[i + 1], pk, x1=x1)
@@ -202,6 +249,7 @@ class ResTrunk:
         return y, (x0, x1, r1, a1, r2, a2, y)
 
     def forward(self, x, params, save, training):
+        self.training = training       # BatchNorm: per-slot batch statistics vs running statistics
         P = list(params)
         p_drop = self.model.dropout_ratio
         drop = training and p_drop > 0
@@ -209,7 +257,10 @@ class ResTrunk:
         h = x
         skips = []
         for k, name in enumerate(self.DOWN):
-            y, st = self._stack_fwd(P, self.slots[name], h)
+            if (name, 1) in self.bn:
+                y, st = self._stack_fwd_bn(P, self.slots[name], name, h)
+            else:
+                y, st = self._stack_fwd(P, self.slots[name], h)
             s[name] = st
             skips.append(y)
             h = K.maxpool2_fwd(y)
@@ -218,7 +269,10 @@ class ResTrunk:
                 m = self._mask("pool%d" % (k + 1), h.shape[0], h.shape[3], p, h.device)
                 K.channel_scale(h, m, out=h)
                 s["pool%d.mask" % (k + 1)] = m
-        y, st = self._stack_fwd(P, self.slots["mid"], h)
+        if ("mid", 1) in self.bn:
+            y, st = self._stack_fwd_bn(P, self.slots["mid"], "mid", h)
+        else:
+            y, st = self._stack_fwd(P, self.slots["mid"], h)
         s["mid"] = st
         for j, name in enumerate(self.UP):
             skip = skips[3 - j]
@@ -264,6 +318,36 @@ class ResTrunk:
             return None, None
         return conv3x3_dgrad(g_z0, P[i], pk, split=split, mask1=mask1)
 
+    def _bn_bwd(self, P, key, z, g, stat, out, grads, add=None, mask=None):
+        j, _ = self.bn[key]
+        o = out(j)
+        dgam = torch.empty_like(P[j]) if o is None else o[0]
+        dbet = torch.empty_like(P[j + 1]) if o is None else o[1]
+        dz = K.bn_bwd(z, g, stat[0], stat[1], P[j], dgam, dbet, add=add, mask=mask)
+        grads[j], grads[j + 1] = dgam, dbet
+        self._ready(j)
+        return dz
+
+    def _stack_bwd_bn(self, P, i, name, st, g, grads, out, need_dx=True, split=None, mask1=None):
+        """g = dL/d(stack output) * (y > 0)."""
+        pk = self.packs
+        for blk in (2, 1):
+            r, n, a, sa = st[blk]
+            ia = i + 2 + 4 * (blk - 1)
+            grads[ia + 2], grads[ia + 3] = conv3x3_wgrad(g, a, out=out(ia + 2))
+            self._ready(ia + 2)
+            ga, _ = conv3x3_dgrad(g, P[ia + 2], pk, mask0=a)
+            grads[ia], grads[ia + 1] = conv3x3_wgrad(ga, n, out=out(ia))
+            self._ready(ia)
+            dn, _ = conv3x3_dgrad(ga, P[ia], pk)
+            # r feeds the BatchNorm and the residual add: dL/dr = BN^T dn + g, times relu's mask
+            g = self._bn_bwd(P, (name, blk), r, dn, sa, out, grads, add=g, mask=r)
+        grads[i], grads[i + 1] = conv3x3_wgrad(g, st["x0"], st["x1"], out=out(i))
+        self._ready(i)
+        if not need_dx:
+            return None, None
+        return conv3x3_dgrad(g, P[i], pk, split=split, mask1=mask1)
+
     def backward(self, s, dlogits, params):
         P = list(params)
         grads = [None] * len(P)
@@ -295,14 +379,20 @@ class ResTrunk:
             grads[i], grads[i + 1] = convT3x3_wgrad(x_in, g_u, out=out(i))
             self._ready(i)
             g = convT3x3_dgrad(g_u, P[i], self.packs, x_in.shape[1:3], mask=x_in)
-        g_p, _ = self._stack_bwd(P, self.slots["mid"], s["mid"], g, grads, out)
+        if ("mid", 1) in self.bn:
+            g_p, _ = self._stack_bwd_bn(P, self.slots["mid"], "mid", s["mid"], g, grads, out)
+        else:
+            g_p, _ = self._stack_bwd(P, self.slots["mid"], s["mid"], g, grads, out)
         for k in range(3, -1, -1):                       # conv4 .. conv1
             m = s.get("pool%d.mask" % (k + 1))
             if m is not None:
                 K.channel_scale(g_p, m, out=g_p)
             g = K.maxpool2_bwd(skips[k], g_p, gskip[k], relu_mask=True, accumulate=True)
             name = self.DOWN[k]
-            g_p, _ = self._stack_bwd(P, self.slots[name], s[name], g, grads, out, need_dx=k > 0)
+            if (name, 1) in self.bn:
+                g_p, _ = self._stack_bwd_bn(P, self.slots[name], name, s[name], g, grads, out, need_dx=k > 0)
+            else:
+                g_p, _ = self._stack_bwd(P, self.slots[name], s[name], g, grads, out, need_dx=k > 0)
         return grads
 
 

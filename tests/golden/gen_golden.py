@@ -21,6 +21,7 @@ Fixtures (each < 2 MB):
   metrics.npz                    fast_iou_metric and RLE encode on fixed masks
   unetp_{bn,bilinear,bn_bilinear}.npz  UNetp(batch_norm / bilinear_upsample) at 64x64: init, two
                                  train-mode forwards (running statistics), grads, eval forward
+  unetpres_bn.npz                UNetpRes(neurons=4, batch_norm=True, dropout 0) at 64x64, the same
 """
 import os
 import sys
@@ -183,6 +184,36 @@ def gen_variants():
             ye, he = net(xs[2], torch.zeros(N, N))
         save("unetp_%s.npz" % tag, xs=t2n(xs), t=t2n(t0), hebb=t2n(hebb0), Y=t2n(y), Hn=t2n(hn), loss=t2n(loss),
              Y2=t2n(y2), Ye=t2n(ye), He=t2n(he), **init, **after1, **after2, **grad_arrays(net, "g."))
+
+
+def gen_unetpres_bn():
+    """Reference UNetpRes(neurons=4, batch_norm=True, dropout_ratio=0) at 64x64 in training mode
+    (residual blocks with BatchNorm, unet_p_res.py:149-153, :171-176): init state, fwd/bwd grads,
+    running statistics after two forwards, eval-mode forward."""
+    N = 64
+    torch.manual_seed(6)
+    net = UNetpRes(1, 1, CPU, neurons=4, dropout_ratio=0.0, rule="oja", nbf=N, batch_norm=True)
+    # the initial state is regenerated from the seed by the test (RNG-order-identical init); only
+    # per-tensor fp64 sums are stored to check that (keeps the fixture < 2 MB)
+    init = {"sum." + k: np.float64(v.double().sum().item()) for k, v in net.state_dict().items()}
+    g = torch.Generator().manual_seed(22)
+    xs = torch.rand(3, 1, 1, N, N, generator=g)
+    t0 = (torch.rand(N, N, generator=g) > 0.5).float()
+    hebb0 = 0.1 * torch.randn(N, N, generator=g)
+    net.train()
+    y, hn = net(xs[0], hebb0)
+    loss = nn.BCELoss()(y.view(-1), t0.view(-1))
+    loss.backward()
+    bufs = lambda pre: {k: v for k, v in sd_arrays(net, pre).items() if "running" in k or "num_batches" in k}  # noqa
+    after1 = bufs("s1.")
+    with torch.no_grad():
+        y2, _ = net(xs[1], hebb0)
+    after2 = bufs("s2.")
+    net.eval()
+    with torch.no_grad():
+        ye, he = net(xs[2], torch.zeros(N, N))
+    save("unetpres_bn.npz", xs=t2n(xs), t=t2n(t0), hebb=t2n(hebb0), Y=t2n(y), Hn=t2n(hn), loss=t2n(loss),
+         Y2=t2n(y2), Ye=t2n(ye), He=t2n(he), **init, **after1, **after2, **grad_arrays(net, "g."))
 
 
 def trunk_from_blocks(base, depth, nbf, rule, seed):
@@ -447,6 +478,7 @@ if __name__ == "__main__":
             globals()[fn]()
         sys.exit(0)
     gen_variants()
+    gen_unetpres_bn()
     gen_head()
     gen_trace_seq()
     gen_unetp_c8()

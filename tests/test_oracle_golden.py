@@ -281,3 +281,43 @@ def test_unetp_bn_batched_slots_equal_sequential():
     for k in a.state_dict():
         if "s2." + k in g:
             close(a.state_dict()[k], g["s2." + k])
+
+
+def test_unetpres_bn_fixture():
+    """UNetpRes(batch_norm=True): residual blocks with BatchNorm (unet_p_res.py:149-153, :171-176),
+    training-mode fwd/bwd, running statistics after two forwards, eval-mode forward."""
+    g = golden("unetpres_bn.npz")
+    torch.manual_seed(6)
+    net = oracle.RefUNetpRes(1, 1, neurons=4, dropout_ratio=0.0, rule="oja", nbf=64, batch_norm=True)
+    for k, v in net.state_dict().items():          # RNG-order-identical init (fp64 sums stored)
+        assert abs(v.double().sum().item() - float(g["sum." + k])) <= 1e-9 * max(1.0, abs(float(g["sum." + k])))
+    net.train()
+    xs = _t(g["xs"])
+    y, hn = net(xs[0], _t(g["hebb"]))
+    loss = oracle.bce_loss(y, _t(g["t"]))
+    loss.backward()
+    close(y, g["Y"])
+    close(hn, g["Hn"])
+    close(loss, g["loss"])
+    for k, p in net.named_parameters():
+        if p.grad is None:
+            assert k == "eta"
+            continue
+        close(p.grad, g["g." + k], rtol=1e-4, atol=1e-7)
+    for k, v in net.state_dict().items():
+        if "s1." + k in g:
+            close(v, g["s1." + k])
+    with torch.no_grad():
+        y2, _ = net(xs[1], _t(g["hebb"]))
+    close(y2, g["Y2"])
+    nbuf = 0
+    for k, v in net.state_dict().items():
+        if "s2." + k in g:
+            close(v, g["s2." + k])
+            nbuf += 1
+    assert nbuf == 3 * 10                           # 5 stacks x 2 residual blocks x 1 BatchNorm2d
+    net.eval()
+    with torch.no_grad():
+        ye, he = net(xs[2], torch.zeros(64, 64))
+    close(ye, g["Ye"])
+    close(he, g["He"])

@@ -177,3 +177,62 @@ def test_unetpres_training_dropout_matches_oracle():
         got, want = p.grad.double().cpu(), pr.grad
         rel = ((got - want).norm() / max(want.norm().item(), 1e-30)).item()
         assert rel < 2e-3, (k, rel)
+
+
+def test_unetpres_batchnorm_golden():
+    """UNetpRes(batch_norm=True) on the HIP path vs the reference's golden vectors: train-mode
+    fwd/bwd, running statistics after two forwards, eval-mode forward."""
+    g = golden("unetpres_bn.npz")
+    torch.manual_seed(6)
+    ref = oracle.RefUNetpRes(1, 1, neurons=4, dropout_ratio=0.0, rule="oja", nbf=64, batch_norm=True)
+    net = UNetpRes(1, 1, DEV, neurons=4, dropout_ratio=0.0, rule="oja", nbf=64, batch_norm=True)
+    net.load_state_dict(ref.state_dict())
+    net.train()
+    xs = torch.from_numpy(g["xs"]).to(DEV)
+    hebb = torch.from_numpy(g["hebb"]).to(DEV)
+    y, hn = net(xs[0], hebb)
+    loss = bce_loss(y, torch.from_numpy(g["t"]).to(DEV))
+    loss.backward()
+    assert_close(y, g["Y"])
+    assert_close(hn, g["Hn"])
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    for k, p in net.named_parameters():
+        if k == "eta":
+            assert p.grad is None
+            continue
+        assert_close(p.grad, torch.from_numpy(g["g." + k]), rtol=1e-3, atol_rel=1e-4)
+    for k, v in net.state_dict().items():
+        if "s1." + k in g:
+            assert_close(v, g["s1." + k])
+    with torch.no_grad():
+        y2, _ = net(xs[1], hebb)
+    assert_close(y2, g["Y2"])
+    for k, v in net.state_dict().items():
+        if "s2." + k in g:
+            assert_close(v, g["s2." + k])
+    net.eval()
+    with torch.no_grad():
+        ye, he = net(xs[2], torch.zeros(64, 64, device=DEV))
+    assert_close(ye, g["Ye"])
+    assert_close(he, g["He"])
+
+
+def test_unetpres_batchnorm_slots_match_oracle():
+    """Three slots in one training step == the oracle's per-slot BatchNorm."""
+    torch.manual_seed(3)
+    ref = oracle.RefUNetpRes(1, 1, neurons=4, dropout_ratio=0.0, rule="hebb", nbf=32, batch_norm=True)
+    net = UNetpRes(1, 1, DEV, neurons=4, dropout_ratio=0.0, rule="hebb", nbf=32, batch_norm=True)
+    net.load_state_dict(ref.state_dict())
+    gen = torch.Generator().manual_seed(5)
+    x = torch.rand(3, 1, 32, 32, generator=gen)
+    t = (torch.rand(3, 32, 32, generator=gen) > 0.5).float()
+    H = 0.1 * torch.randn(3, 32, 32, generator=gen)
+    yr, hr = ref(x, H)
+    oracle.bce_loss(yr, t).backward()
+    y, h = net(x.to(DEV), H.to(DEV))
+    bce_loss(y, t.to(DEV)).backward()
+    assert_close(y, yr)
+    assert_close(h, hr)
+    rsd = ref.state_dict()
+    for k, v in net.state_dict().items():
+        assert_close(v, rsd[k])
