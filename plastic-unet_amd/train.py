@@ -8,7 +8,7 @@ save checkpoints (:153-203).  Differences, all opt-in:
   --hebb-mode sequential   one trace threaded through the B samples of each step in order
   --batch-norm / --bilinear  the reference constructor flags batch_norm / bilinear_upsample
   --model-type     unetpres (reference default) | unetp, with --depth/--base-ch for UNetp
-  --synthetic N / --dataset FILE.npz   input data (the TGS PNG loader needs skimage, absent here)
+  --synthetic N / --dataset FILE.npz   input data besides --data DIR (the TGS PNG layout, utils/data_set.py)
 Data-parallel training: launch with torch.distributed.run; each rank trains its contiguous shard
 of every global batch and gradients are averaged over RCCL.
 Checkpoints: ``{out}/train[_{epoch}]_net.pth`` (state_dict, reference keys) and the HDF5 payload of
@@ -183,6 +183,8 @@ def parse_args(argv=None):
     parser.add_option('--img-size', dest='img_size', type='int', default=101)
     parser.add_option('--batch-size', dest='batch_size', type='int', default=1)
     parser.add_option('--synthetic', dest='synthetic', type='int', default=0, help='N synthetic samples')
+    parser.add_option('--val-ratio', dest='val_ratio', type='float', default=0.2,
+                      help='validation share of the TGS split (data_set.py: test_size)')
     parser.add_option('--hebb-mode', dest='hebb_mode', default='slots',
                       help="slots: one trace per batch slot; sequential: one trace threaded through the batch")
     parser.add_option('--batch-norm', dest='batch_norm', action='store_true', default=False)
@@ -204,8 +206,10 @@ def load_data(args):
     if args.dataset_file:
         d = np.load(args.dataset_file)
         return d["x_train"], d["x_valid"], d["y_train"], d["y_valid"]
-    raise ValueError("The input data directory or dataset file not specified (the TGS PNG loader needs "
-                     "skimage; use --dataset FILE.npz or --synthetic N)")
+    if args.data_dir:           # the TGS layout (train.csv, depths.csv, train/{images,masks}/*.png)
+        from utils import load_train_dataset
+        return load_train_dataset(args.data_dir, S, S, 1, val_ratio=args.val_ratio, debug=args.debug)
+    raise ValueError("The input data directory or dataset file not specified")
 
 
 if __name__ == '__main__':

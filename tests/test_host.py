@@ -27,3 +27,52 @@ def test_batches_shard_contiguously():
     assert list(train._batches(10, 2, 1, 0)) == [(0, 2), (2, 4), (4, 6), (6, 8), (8, 10)]
     assert list(train._batches(10, 2, 2, 1)) == [(2, 4), (6, 8)]          # rank 1 of 2, drop ragged tail
     assert list(train._batches(3, 1, 1, 0)) == [(0, 1), (1, 2), (2, 3)]     # the reference's bs=1 loop
+
+
+def _fake_tgs(root, n=30, size=101, seed=0):
+    """A TGS-layout directory: train.csv / depths.csv, RGB 8-bit images, 16-bit masks."""
+    import os
+    from PIL import Image
+    rng = np.random.RandomState(seed)
+    os.makedirs(os.path.join(root, "train", "images"))
+    os.makedirs(os.path.join(root, "train", "masks"))
+    ids = ["id%03d" % i for i in range(n)]
+    with open(os.path.join(root, "train.csv"), "w") as f:
+        f.write("id,rle_mask\n" + "".join("%s,\n" % i for i in ids))
+    with open(os.path.join(root, "depths.csv"), "w") as f:
+        f.write("id,z\n" + "".join("%s,%d\n" % (i, rng.randint(50, 900)) for i in ids + ["test0"]))
+    for k, i in enumerate(ids):
+        g = rng.randint(0, 256, (size, size)).astype(np.uint8)
+        Image.fromarray(np.stack([g, g, g], -1)).save(os.path.join(root, "train", "images", i + ".png"))
+        cov = (0.0, 0.45, 1.0)[k % 3]              # three coverage classes, 10 images each (stratified split)
+        m = (rng.rand(size, size) < cov).astype(np.uint16) * 65535
+        Image.fromarray(m).save(os.path.join(root, "train", "masks", i + ".png"))
+    return ids
+
+
+def test_tgs_loader_layout_split_and_resize(tmp_path):
+    """utils.load_train_dataset (data_set.py:18-70 restated): shapes, [0,1] grey images, binary
+    masks, the stratified random_state=42 split, and the skimage-resize restatement."""
+    from utils import load_train_dataset, data_set
+    root = str(tmp_path / "tgs")
+    _fake_tgs(root)
+    xt, xv, yt, yv = load_train_dataset(root, 128, 128, 1, val_ratio=0.2)
+    assert xt.shape == (24, 1, 128, 128) and xv.shape == (6, 1, 128, 128)
+    assert yt.shape == (24, 1, 128, 128) and yv.shape == (6, 1, 128, 128)
+    assert 0.0 <= xt.min() and xt.max() <= 1.0
+    # same size -> no resize: a 101x101 load returns the grey image exactly
+    x101, _, y101, _ = load_train_dataset(root, 101, 101, 1, val_ratio=0.2)
+    assert set(np.unique(y101)) <= {0.0, 1.0}
+    from PIL import Image
+    import os
+    g = np.asarray(Image.open(os.path.join(root, "train", "images", "id000.png")).convert("RGB"), np.float64) / 255
+    grey = g[..., 0] * 0.2125 + g[..., 1] * 0.7154 + g[..., 2] * 0.0721
+    assert any(np.allclose(x[0], grey) for x in x101)
+    # resize restatement: interior pixels are bilinear samples at (r + .5) * s - .5, edges fade to 0
+    img = np.arange(12, dtype=np.float64).reshape(3, 4)
+    r = data_set.resize_bilinear_constant(img, (6, 8))
+    assert r.shape == (6, 8)
+    # output (2, 3) samples (y, x) = (0.75, 1.25): rows 0/1 weighted .25/.75, columns 1/2 .75/.25
+    assert abs(r[2, 3] - (0.25 * (0.75 * img[0, 1] + 0.25 * img[0, 2]) + 0.75 * (0.75 * img[1, 1] + 0.25 * img[1, 2]))) < 1e-12
+    assert abs(r[0, 0] - 0.75 * 0.75 * img[0, 0]) < 1e-12          # (-0.25, -0.25): 3 of 4 neighbours are cval 0
+    assert data_set.cov_to_class(0.0) == 0 and data_set.cov_to_class(0.35) == 4 and data_set.cov_to_class(1.0) == 10
