@@ -11,10 +11,12 @@ save checkpoints (:153-203).  Differences, all opt-in:
   --synthetic N / --dataset FILE.npz   input data besides --data DIR (the TGS PNG layout, utils/data_set.py)
 Data-parallel training: launch with torch.distributed.run; each rank trains its contiguous shard
 of every global batch and gradients are averaged over RCCL.
-Checkpoints: ``{out}/train[_{epoch}]_net.pth`` (state_dict, reference keys) and the HDF5 payload of
-:178-196 under the same keys in ``{out}/train[_{epoch}]_data.npz`` (h5py is not installed).
+Checkpoints: ``{out}/train[_{epoch}]_net.pth`` (state_dict, reference keys), the training parameters
+pickled to ``_parameters.dat`` (:199-200), and the HDF5 payload of :178-196 under the same keys in
+``{out}/train[_{epoch}]_data.npz`` (h5py is not installed).
 """
 import os
+import pickle
 import sys
 import time
 from datetime import datetime
@@ -114,6 +116,8 @@ def train(net, X_train, X_val, y_train, y_val, params):
                 "validation/train_losses": np.asarray(val_train_losses),
                 "validation/test_losses": np.asarray(val_test_losses),
                 "validation/accuracies": np.asarray(val_accuracies)})
+            with open(prefix + "_parameters.dat", "wb") as fo:      # train.py:199-200
+                pickle.dump({k: (str(v) if isinstance(v, torch.device) else v) for k, v in params.items()}, fo)
             torch.save(net.state_dict(), prefix + "_net.pth")
         if terminate:
             if verbose:
