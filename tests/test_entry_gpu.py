@@ -1,0 +1,84 @@
+"""The reference's entry points on the HIP path: train.train() against the reference's own train()
+capture (tests/golden/train_capture.npz: 2 epochs, 3 + 1 samples, 32x32, losses / validation /
+final parameters), eval_net and the infer predict() (threshold -> RLE -> CSV) against the oracle."""
+import csv
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from unet import UNetp  # noqa: E402
+import oracle  # noqa: E402
+from conftest import golden  # noqa: E402
+
+DEV = torch.device("cuda")
+
+
+def _net_from(g, prefix):
+    net = UNetp(1, 1, DEV, rule="oja", nbf=32)
+    net.load_state_dict({k[len(prefix):]: torch.from_numpy(np.asarray(v)) for k, v in g.items()
+                         if k.startswith(prefix)})
+    return net
+
+
+def test_train_matches_reference_train_capture(tmp_path):
+    import train
+    g = golden("train_capture.npz")
+    net = _net_from(g, "init.")
+    params = {"out_dir": str(tmp_path), "device": DEV, "epochs": 2, "stop_time": -1, "lr": 3e-4,
+              "val_every": 1, "save_every": 100, "rollout": 50000, "gamma": 0.666, "steplr": 4,
+              "debug": False, "batch_size": 1}
+    losses, v_train, v_test, v_acc = train.train(net, g["X_train"], g["X_val"], g["y_train"], g["y_val"], params)
+    np.testing.assert_allclose(losses, g["all_losses"], rtol=1e-4)
+    np.testing.assert_allclose(v_train, g["val_train_losses"], rtol=1e-4)
+    np.testing.assert_allclose(v_test, g["val_test_losses"], rtol=1e-4)
+    np.testing.assert_allclose(v_acc, g["val_accuracies"], atol=2e-3)
+    # First-step gradients agree to < 1e-6 relative with identical exact zeros
+    # (tools/diag_train_capture.py); later steps differ where a pre-activation within fp32 noise of
+    # 0 takes the other ReLU branch, which can wake a dead channel and Adam then moves all of its
+    # ~0-gradient weights by O(lr).  So: no coordinate further than 6 Adam steps
+    # (2 lr each) from the reference, and the whole parameter vector within 2e-3 relative L2.
+    diff2, ref2 = 0.0, 0.0
+    for k, v in net.state_dict().items():
+        ref = torch.from_numpy(np.asarray(g["final." + k]))
+        d = (v.cpu() - ref).abs()
+        assert d.max().item() <= 6 * 2 * 3e-4, (k, d.max().item())
+        diff2 += float((d.double() ** 2).sum())
+        ref2 += float((ref.double() ** 2).sum())
+    assert (diff2 / ref2) ** 0.5 <= 2e-3
+    # checkpoint files of train.py:178-203 (state_dict loads back into the reference-keyed model)
+    for f in ("train_net.pth", "train_data.npz", "train_parameters.dat"):
+        assert os.path.exists(os.path.join(str(tmp_path), f)), f
+    sd = torch.load(os.path.join(str(tmp_path), "train_net.pth"), weights_only=True)
+    ref_net = oracle.RefUNetp(1, 1, rule="oja", nbf=32)
+    ref_net.load_state_dict(sd)
+
+
+def test_eval_and_predict_match_oracle(tmp_path):
+    import eval as ev
+    import infer
+    g = golden("train_capture.npz")
+    net = _net_from(g, "final.")
+    ref = oracle.RefUNetp(1, 1, rule="oja", nbf=32)
+    ref.load_state_dict({k[6:]: torch.from_numpy(np.asarray(v)) for k, v in g.items() if k.startswith("final.")})
+    X = np.concatenate([g["X_train"], g["X_val"]])
+    Y = np.concatenate([g["y_train"], g["y_val"]])
+    acc, loss = ev.eval_net(net, X, Y, DEV, batch=3)
+    racc, rloss = oracle.ref_eval_net(ref, X, Y)
+    assert abs(loss - rloss) < 1e-5 * abs(rloss)
+    assert abs(acc - racc) < 2e-3
+    rows = infer.predict(net, ["a", "b", "c", "d"], X, {"device": DEV, "mask_threshold": 0.5,
+                                                        "out_dir": str(tmp_path)})
+    with open(os.path.join(str(tmp_path), "submission.csv")) as f:
+        got = list(csv.reader(f))
+    assert got[0] == ["id", "rle_mask"] and len(got) == 5
+    with torch.no_grad():
+        for (i, rle), x in zip(rows, X):
+            y, _ = ref(torch.from_numpy(x[None].astype(np.float32)), ref.initialZeroHebb())
+            m = y.numpy() > 0.5
+            far = np.abs(y.numpy() - 0.5) > 1e-5          # masks bit-exact away from the threshold
+            yg = infer.predict_masks(net, x[None], DEV)[0] > 0.5
+            assert np.array_equal(yg[far], m[far])
