@@ -258,18 +258,24 @@ __device__ __forceinline__ void wg_split3(const float (&x)[8], wg_bf16x8& h, wg_
 // X6: the 16 staged pixel rows are one k-step of v_mfma_f32_32x32x16_bf16 and each fp32 product
 // is 6 exact bf16 products (hi/mid/lo split, fp32 accumulation) - 6 x 32 cycles against the
 // 8 x 64 of v_mfma_f32_32x32x2_f32; lane (i, h) reads rows 8h..8h+7 of its column.
-template <int BN, int BK, int WN, int WK, int NBUF, bool X6>
-__global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
+// NW waves (WN x WK): 6 waves give the 64 x 576 tile of the 64-channel layers (K = 9 x 64 or
+// 9 x 128 with no padding, 64 x 96 per wave: 5 operand splits per 36 MFMAs); the P pieces that do
+// not divide among the waves are issued by every wave anyway (the counted wait stays uniform),
+// the surplus ones reading the zero page into a 1 KB sink.
+template <int BN, int BK, int WN, int WK, int NBUF, bool X6, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void wgrad_dma_kernel(const WgradParams p) {
     constexpr int FN = BN / WN / 32;
     constexpr int FK = BK / WK / 32;
     constexpr int P_ROWS = 256 / BN;              // rows per 1 KB glds instruction
-    constexpr int P_LD = WG_BM / P_ROWS / 4;      // glds per wave per stage
-    constexpr int Q_LD = WG_BM * BK / 1024;       // Q instructions may straddle rows (BK = 192)
+    constexpr int P_TOT = WG_BM / P_ROWS;         // P glds per stage
+    constexpr int P_LD = (P_TOT + NW - 1) / NW;   // per wave (surplus -> sink)
+    constexpr int Q_LD = WG_BM * BK / 256 / NW;   // Q instructions may straddle rows (BK = 192)
     constexpr int G = P_LD + Q_LD;
     constexpr int STAGE = WG_BM * (BN + BK);
-    static_assert(WN * WK == 4 && P_LD >= 1 && Q_LD >= 1 && 256 % BN == 0 && (WG_BM * BK) % 1024 == 0, "tile");
+    constexpr int SINK = (P_TOT % NW) ? 256 : 0;
+    static_assert(WN * WK == NW && P_LD >= 1 && Q_LD >= 1 && 256 % BN == 0 && (WG_BM * BK) % (256 * NW) == 0, "tile");
 
-    __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE];
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE + SINK];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -319,11 +325,14 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
         float* qs = ps + WG_BM * BN;
 #pragma unroll
         for (int j = 0; j < P_LD; ++j) {
-            const int row0 = (wave * P_LD + j) * P_ROWS;
+            const int I = (P_TOT % NW) ? wave + NW * j : wave * P_LD + j;
+            const int row0 = I * P_ROWS;
             const int m = m0 + row0 + p_dr;
             const float* g = g_wg_zero16;
-            if (m < m_end && p_in) g = p.P + (long long)m * p.N + pn;
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(ps + row0 * BN), 16, 0, 0);
+            float* dst = ps + row0 * BN;
+            if (SINK && I >= P_TOT) dst = lds + NBUF * STAGE;
+            else if (m < m_end && p_in) g = p.P + (long long)m * p.N + pn;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)dst, 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < Q_LD; ++j) {
@@ -371,8 +380,7 @@ __global__ __launch_bounds__(256) void wgrad_dma_kernel(const WgradParams p) {
     for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(m_begin + s0 * WG_BM, s0);
 
     for (int t = 0; t < T; ++t) {
-        if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
         __builtin_amdgcn_s_barrier();
         const float* ps = lds + (t % NBUF) * STAGE;
         const float* qs = ps + WG_BM * BN;
@@ -690,6 +698,13 @@ static bool small_wgrad_ok(const pu_wgrad_args* a) {
 #ifndef PU_WG_X6_BK256
 #define PU_WG_X6_BK256 1
 #endif
+#ifndef PU_WG_X6_W6
+#define PU_WG_X6_W6 0      // 6-product 64-channel layers with K % 576 == 0 on 64 x 576 tiles, 6 waves: measured
+                           // 6% slower (6 waves on 4 SIMDs; NBUF 2 for two blocks per CU: 15% slower)
+#endif
+#ifndef PU_WG_W6_NBUF
+#define PU_WG_W6_NBUF 3    // its LDS ring depth (3: 121 KB, one block per CU; 2: 80 KB, two)
+#endif
 static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     PU_REQUIRE(a && a->batch > 0 && a->out_h > 0 && a->out_w > 0 && a->in_h > 0 && a->in_w > 0, "pu_wgrad: bad grid");
     PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0, "pu_wgrad: bad taps");
@@ -750,6 +765,10 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
         ceil_div(ext_k, 256) * 256 <= ceil_div(ext_k, 128) * 128) {
         pl->BK = 256;
         occ = 2;
+    }
+    if (PU_WG_X6_W6 && a->math == 1 && pl->dma && pl->BN == 64 && a->bias_mode != 2 && ext_k % 576 == 0) {
+        pl->BK = 576;
+        occ = PU_WG_W6_NBUF == 3 ? 1 : 2;
     }
     pl->gx = ceil_div(ext_k, pl->BK);
     pl->gy = ceil_div(ext_n, pl->BN);
@@ -1123,6 +1142,10 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
             else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
             else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
             else if (pl.BK == 256) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true>), grid, dim3(256), 0, s, p);
+            else if (pl.BK == 576) {   // bias mode 1 only (its 64 P columns fit the 384 threads)
+                PU_REQUIRE(a->bias_mode != 2, "pu_wgrad: 64 x 576 tile with a column bias");
+                hipLaunchKernelGGL((wgrad_dma_kernel<64, 576, 1, 6, PU_WG_W6_NBUF, true, 6>), grid, dim3(384), 0, s, p);
+            }
             else PU_WG_DMA(128, 128, 2, 2);
         } else if (pl.qvec) {
             if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, true);

@@ -51,6 +51,7 @@ CONV_CASES = [
     (1, 4, 4, 64, 64, 40),      # tiny M, 64x64 tile, split-K (fwd + dgrad with the n0 split)
     (2, 8, 8, 48, 0, 64),       # wgrad 64x128 tile, ragged last k-tile, bias column sums
     (1, 8, 8, 64, 64, 32),      # wgrad 64x128 tile, two sources
+    (2, 9, 13, 64, 64, 64),     # wgrad 64x576 6-wave tile (K = 2 x 576), two sources, ragged pixels
     (2, 37, 45, 16, 0, 16),     # small-channel direct kernels: several 16x32 tiles, ragged edges
     (1, 19, 70, 4, 4, 4),       # small-channel, two 4-channel sources, N = 4
 ]
