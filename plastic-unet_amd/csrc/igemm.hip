@@ -624,6 +624,9 @@ __device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf
 #define PU_X6_W41 1      // 128x128 tile as 4 waves along M (each 32 pixels x 128 channels): one pixel
                          // split feeds 4 weight fragments (24 MFMAs), 2x2 waves split twice as much
 #endif
+#ifndef PU_X6_PF
+#define PU_X6_PF 0       // 1: register-prefetched pipeline (stage ts+1 fragments read during stage ts MFMAs)
+#endif
 #ifndef PU_X6_ORDER
 #define PU_X6_ORDER 0    // 0: per pixel fragment split + 6 FN MFMAs; 1: all splits first, term-major MFMAs
 #endif
@@ -750,8 +753,76 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
     const int swz = (lr >> 2) & 3;
     const int pos0 = ((2 * lh) ^ swz) * 4, pos1 = ((2 * lh + 1) ^ swz) * 4;
 
+#if PU_X6_PF
+    // Register-prefetched pipeline: the fragments of stage ts+1 are read from LDS right after the
+    // barrier of iteration ts and land while the MFMAs of stage ts (already in registers) run, so
+    // neither the barrier nor the LDS latency sits in front of an MFMA cluster.  Stage ts+3 is
+    // issued into the slot stage ts was read from (every wave waited for those reads before the
+    // barrier).  Requires KSUB == 1, NBUF == 3.
+    static_assert(KSUB == 1 && NBUF == 3, "PF pipeline");
+    struct Frag {
+        f32x4 xa[FM], xb[FM];
+        bf16x8_t fw[3][FN];
+    };
+    auto read_frags = [&](int ts, Frag& f) {
+        const float* a = lds + (ts % NBUF) * STAGE;
+        const float* wp = a + A_FL;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            f.xa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos0);
+            f.xb[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos1);
+        }
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+                f.fw[pl][j] = *reinterpret_cast<const bf16x8_t*>(wp + ((pl * 2 + lh) * BN + b_row0 + j * 32) * 4);
+    };
+    auto mfmas = [&](const Frag& f) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            bf16x8_t xh, xm, xl;
+            split3_bf16(f.xa[i], f.xb[i], xh, xm, xl);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                f32x16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[1][j], xm, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[2][j], xh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[0][j], xl, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[1][j], xh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[0][j], xm, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[0][j], xh, c, 0, 0, 0);
+                acc[i][j] = c;
+            }
+        }
+    };
+    auto step = [&](int ts, const Frag& cur, Frag& nxt) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");   // stage ts+1 landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         // my reads of slot ts done
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read_frags(ts + 1, nxt);
+        issue(ts + 3, ts % NBUF);
+        mfmas(cur);
+    };
+#pragma unroll
+    for (int s0 = 0; s0 < NBUF; ++s0) issue(s0, s0);
+    Frag f0, f1;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_frags(0, f0);
+    int ts = 0;
+    for (; ts + 1 < TS; ts += 2) {
+        step(ts, f0, f1);
+        step(ts + 1, f1, f0);
+    }
+    if (ts < TS) mfmas(f0);
+    if (false)
+#else
 #pragma unroll
     for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(s0, s0);
+#endif
 
     for (int ts = 0; ts < TS; ++ts) {
         // ring slot ts landed when only the NBUF-2 younger slots' loads are pending
@@ -1069,6 +1140,9 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
 #ifndef PU_X6_TILES
 #define PU_X6_TILES 1
 #endif
+#ifndef PU_X6_N64
+#define PU_X6_N64 0      // N <= 64 layers: 0 = 256x64 (4 waves), 1 = 512x64 (8 waves), 2 = 128x64 (4x1 waves)
+#endif
 #ifndef PU_X6_BIG
 #define PU_X6_BIG 1      // long-K layers (k_pad >= 2048): 1 = 256x128 8-wave tiles, 2 = also 256x256
                          // for N >= 256 (measured slower); 0 = 128x128 4-wave tiles everywhere
@@ -1086,6 +1160,8 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
     if (N <= 64) {
         *bn = 64;
         *bm = blocks_for(M, N, 256, 64) >= 480 ? 256 : 128;
+        if (PU_X6_N64 == 1 && blocks_for(M, N, 512, 64) >= 480) { *bm = 512; target = 256; }
+        if (PU_X6_N64 == 2) *bm = 128;   // launched as 4 x 1 waves
     } else if (PU_X6_BIG && a->k_pad >= 2048) {
         // 8 waves, one block per CU (85 KB of LDS), each wave 32 pixels x 128 channels: fewer
         // LDS-DMA pieces and global bytes per MFMA than two 128 x 128 blocks; +2-4% on the
@@ -1210,6 +1286,7 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         p.t_per = a->k_pad / IG_BK;
     }
     p.part = (float*)a->workspace;
+    const bool w41_64 = PU_X6_N64 == 2 && bm == 128 && bn == 64;
     const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
     if (a->weight6 && mode == LOAD_CHUNK16 && !PU_NO_DMA) {
         p.wt = reinterpret_cast<const float*>(a->weight6);
@@ -1219,7 +1296,10 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
             hipLaunchKernelGGL((igemm_x6_kernel<256, 256, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
         else if (bm == 256 && bn == 128)
             hipLaunchKernelGGL((igemm_x6_kernel<256, 128, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
+        else if (bm == 512)
+            hipLaunchKernelGGL((igemm_x6_kernel<512, 64, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
         else if (bm == 256) PU_X6(256, 64, 4, 1);
+        else if (w41_64) PU_X6(128, 64, 4, 1);
         else if (bm == 128 && bn == 128) {
             if (PU_X6_W41) PU_X6(128, 128, 4, 1);
             else PU_X6(128, 128, 2, 2);

@@ -262,7 +262,11 @@ __device__ __forceinline__ void wg_split3(const float (&x)[8], wg_bf16x8& h, wg_
 // 9 x 128 with no padding, 64 x 96 per wave: 5 operand splits per 36 MFMAs); the P pieces that do
 // not divide among the waves are issued by every wave anyway (the counted wait stays uniform),
 // the surplus ones reading the zero page into a 1 KB sink.
-template <int BN, int BK, int WN, int WK, int NBUF, bool X6, int NW = 4>
+// FQ: stride 1, same-size input (Hi == Ho, Wi == Wo >= 4) - a Q lane's source row is its output
+// pixel m shifted by the tap, so the per-stage address is one scalar product plus per-lane
+// constants, and the lane's (ho, wo) advance by compare-and-wrap (row delta < 4 < Wo) instead of
+// the per-lane divisions of the general path.
+template <int BN, int BK, int WN, int WK, int NBUF, bool X6, int NW = 4, bool FQ = false>
 __global__ __launch_bounds__(NW * 64) void wgrad_dma_kernel(const WgradParams p) {
     constexpr int FN = BN / WN / 32;
     constexpr int FK = BK / WK / 32;
@@ -319,6 +323,20 @@ __global__ __launch_bounds__(NW * 64) void wgrad_dma_kernel(const WgradParams p)
             q_cs[j] = first ? p.c0 : p.c1;
         }
     }
+    // FQ lane constants: source = q_ptr + (m + dr + (r - pad) * Wi + (s - pad)) * cs
+    const float* q_fb[FQ ? Q_LD : 1];
+    bool q_first[FQ ? Q_LD : 1];
+    if constexpr (FQ) {
+#pragma unroll
+        for (int j = 0; j < Q_LD; ++j) {
+            q_first[j] = q_cs[j] == p.c0;
+            q_fb[j] = q_ptr[j] ? q_ptr[j] + (long long)(q_dr[j] + (q_r[j] - p.pad) * p.Wi + (q_s[j] - p.pad)) * q_cs[j]
+                               : g_wg_zero16;
+            q_r[j] -= p.pad;
+            q_s[j] -= p.pad;
+        }
+    }
+    const float* p_lane = p.P + (long long)p_dr * p.N + pn;
 
     auto issue = [&](int m0, int slot) {
         float* ps = lds + slot * STAGE;
@@ -331,7 +349,7 @@ __global__ __launch_bounds__(NW * 64) void wgrad_dma_kernel(const WgradParams p)
             const float* g = g_wg_zero16;
             float* dst = ps + row0 * BN;
             if (SINK && I >= P_TOT) dst = lds + NBUF * STAGE;
-            else if (m < m_end && p_in) g = p.P + (long long)m * p.N + pn;
+            else if (m < m_end && p_in) g = p_lane + (long long)(m0 + row0) * p.N;
             __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)dst, 16, 0, 0);
         }
 #pragma unroll
@@ -341,6 +359,20 @@ __global__ __launch_bounds__(NW * 64) void wgrad_dma_kernel(const WgradParams p)
             const int wou = mu - tu * p.Wo;
             const int bu = fdiv(tu, p.dHo);
             const int hou = tu - bu * p.Ho;
+            if constexpr (FQ) {
+                int wo = wou + q_dr[j];
+                const bool cw = wo >= p.Wo;
+                wo = cw ? wo - p.Wo : wo;
+                int ho = hou + (cw ? 1 : 0);
+                ho = ho >= p.Ho ? ho - p.Ho : ho;
+                const int hi = ho + q_r[j], wi = wo + q_s[j];
+                const bool ok = mu + q_dr[j] < m_end && q_ptr[j] && (unsigned)hi < (unsigned)p.Hi &&
+                                (unsigned)wi < (unsigned)p.Wi;
+                const long long mo = q_first[j] ? (long long)mu * p.c0 : (long long)mu * p.c1;
+                const float* g = ok ? q_fb[j] + mo : g_wg_zero16;
+                __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(qs + (wave * Q_LD + j) * 256), 16, 0, 0);
+                continue;
+            }
             // lane delta with carry, branch-free (keeps the main loop one basic block)
             int wo = wou + q_dr[j];
             const int cw = fdiv(wo, p.dWo);
@@ -702,6 +734,12 @@ static bool small_wgrad_ok(const pu_wgrad_args* a) {
 #define PU_WG_X6_W6 0      // 6-product 64-channel layers with K % 576 == 0 on 64 x 576 tiles, 6 waves: measured
                            // 6% slower (6 waves on 4 SIMDs; NBUF 2 for two blocks per CU: 15% slower)
 #endif
+#ifndef PU_WG_FQ
+#define PU_WG_FQ 1         // stride-1 same-size layers: scalar + compare-and-wrap Q addressing
+#endif
+#ifndef PU_WG_X6_W3
+#define PU_WG_X6_W3 0      // 6-product 64-channel layers with K % 192 == 0 on 64 x 192 tiles as 3 waves of 64 x 64
+#endif
 #ifndef PU_WG_W6_NBUF
 #define PU_WG_W6_NBUF 3    // its LDS ring depth (3: 121 KB, one block per CU; 2: 80 KB, two)
 #endif
@@ -770,7 +808,11 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
         pl->BK = 576;
         occ = PU_WG_W6_NBUF == 3 ? 1 : 2;
     }
-    pl->gx = ceil_div(ext_k, pl->BK);
+    if (PU_WG_X6_W3 && a->math == 1 && pl->dma && pl->BN == 64 && ext_k % 192 == 0) {
+        pl->BK = -192;   // marker: the 3-wave kernel (tile width 192)
+        occ = 4;
+    }
+    pl->gx = ceil_div(ext_k, pl->BK < 0 ? -pl->BK : pl->BK);
     pl->gy = ceil_div(ext_n, pl->BN);
     const int tiles = pl->gx * pl->gy;
     // one full round of resident blocks: a grid a few blocks past a multiple of the resident
@@ -1085,7 +1127,7 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
     int st = plan_wgrad(a, &pl);
     if (st != PU_OK) return st;
     if (bn) *bn = pl.BN;
-    if (bk) *bk = pl.BK;
+    if (bk) *bk = pl.BK < 0 ? -pl.BK : pl.BK;
     if (qvec) *qvec = pl.small ? 2 : (pl.qvec ? 1 : 0);   // 2: small-channel direct kernel
     if (splits) *splits = pl.splits;
     return PU_OK;
@@ -1130,10 +1172,12 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
         phase &= ~1;
     }
     dim3 grid(p.gx * p.gy * pl.splits);
+    const bool fq = PU_WG_FQ && a->stride == 1 && a->in_h == a->out_h && a->in_w == a->out_w && a->out_w >= 4;
     if (phase & 1) {
 #define PU_WG_DMA(BN_, BK_, WN_, WK_)                                                                    \
     do {                                                                                                     \
-        if (a->math == 1) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, true>), grid, dim3(256), 0, s, p); \
+        if (a->math == 1 && fq) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, true, 4, true>), grid, dim3(256), 0, s, p); \
+        else if (a->math == 1) hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, true>), grid, dim3(256), 0, s, p); \
         else hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, false>), grid, dim3(256), 0, s, p); \
     } while (0)
 #define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
@@ -1141,7 +1185,12 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
             if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
             else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
             else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
+            else if (pl.BK == 256 && fq) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true, 4, true>), grid, dim3(256), 0, s, p);
             else if (pl.BK == 256) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true>), grid, dim3(256), 0, s, p);
+            else if (pl.BK == -192) {   // 64 x 192 as 3 waves of 64 x 64 (x6, PU_WG_X6_W3)
+                if (fq) hipLaunchKernelGGL((wgrad_dma_kernel<64, 192, 1, 3, 3, true, 3, true>), grid, dim3(192), 0, s, p);
+                else hipLaunchKernelGGL((wgrad_dma_kernel<64, 192, 1, 3, 3, true, 3>), grid, dim3(192), 0, s, p);
+            }
             else if (pl.BK == 576) {   // bias mode 1 only (its 64 P columns fit the 384 threads)
                 PU_REQUIRE(a->bias_mode != 2, "pu_wgrad: 64 x 576 tile with a column bias");
                 hipLaunchKernelGGL((wgrad_dma_kernel<64, 576, 1, 6, PU_WG_W6_NBUF, true, 6>), grid, dim3(384), 0, s, p);
