@@ -12,6 +12,7 @@
 // a single ds_read_b128 and feeds them to 4 MFMAs: for MFMA step s, lane (i, h) supplies
 // A[i][kk*8 + 4h + s] and B[kk*8 + 4h + s][j] - the same k on both operands, so the sum is exact.
 #include "common.h"
+#include <type_traits>
 
 // Experimental ablations for performance analysis (tools/ablate.sh); 0 in the product build.
 //   1: no global loads in the K loop (LDS tiles keep stale data)   2: no LDS staging stores
@@ -54,6 +55,7 @@ struct IgemmParams {
     const float* resid;     // RESID: NHWC tensor shaped like dst0, added before ReLU / mask
     int shuf_h, shuf_w, shuf_off;   // SHUFFLE2 output grid and crop offset
     FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
+    int in_pix;             // batch * Hi * Wi (lean kernel's buffer extent)
 };
 
 // Load 4 consecutive k values (k, k+1, k+2, k+3) of GEMM row (pb, hb, wb) into v.
@@ -920,6 +922,263 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
     }
 }
 
+// ---------------------------------------------------------------- lean 6-product kernel
+// The same GEMM, tiles, LDS images, MFMA sequence and epilogue as igemm_x6_kernel, re-shaped to
+// issue few instructions per K stage (PMC on the top 64-channel layer: ~130 VALU + ~95 SALU per
+// 24 MFMAs per wave - the waves were issue-bound, MFMA busy 0.43):
+//   * loads are buffer_load ... lds through buffer descriptors: per-lane byte offsets are
+//     precomputed once per block for every tap (an out-of-image tap gets an out-of-range offset:
+//     the range check writes zeros into LDS - probed, tools/probes/oob_lds.hip), the stage's
+//     (tap, channel) offset is one scalar soffset;
+//   * the 9 taps x CG channel halves of a channel group are unrolled, so the tap, the ring slot
+//     and every LDS address are compile-time constants;
+//   * the 3-term split is written pair-wise (v_cvt_pk_bf16_f32 + v_pk_add_f32: 4.5 VALU/element).
+// Requirements (host: lean_ok): 3x3 taps, K order cgroup 16 (CG 1) or 32 (CG 2), c1 == 0 or
+// c1 == c0 (one pixel stride for both sources), K == k_pad, split-K on group boundaries,
+// every tensor under 2 GB.
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, F, I + 1>(static_cast<F&&>(f));
+    }
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+constexpr unsigned LEAN_OOB = 0x80000000u;
+
+__device__ __forceinline__ unsigned pk_bf16(f32x2 v) {
+    const bf16x2_t h = __builtin_convertvector(v, bf16x2_t);
+    return __builtin_bit_cast(unsigned, h);
+}
+
+// x = hi + mid + lo exactly (round-to-nearest at each step), 8 elements as 4 pairs
+__device__ __forceinline__ void split3_pairs(const f32x4 lo4, const f32x4 hi4, bf16x8_t& h, bf16x8_t& m, bf16x8_t& l) {
+#pragma clang fp contract(off)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 hv, mv, lv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const f32x2 x = q < 2 ? f32x2{lo4[2 * q], lo4[2 * q + 1]} : f32x2{hi4[2 * q - 4], hi4[2 * q - 3]};
+        const unsigned a = pk_bf16(x);
+        const f32x2 af = {__builtin_bit_cast(float, a << 16), __builtin_bit_cast(float, a & 0xffff0000u)};
+        const f32x2 r = x - af;
+        const unsigned b = pk_bf16(r);
+        const f32x2 bf = {__builtin_bit_cast(float, b << 16), __builtin_bit_cast(float, b & 0xffff0000u)};
+        const f32x2 c = r - bf;
+        hv[q] = a;
+        mv[q] = b;
+        lv[q] = pk_bf16(c);
+    }
+    h = __builtin_bit_cast(bf16x8_t, hv);
+    m = __builtin_bit_cast(bf16x8_t, mv);
+    l = __builtin_bit_cast(bf16x8_t, lv);
+}
+
+// buffer_load_dwordx4 ... lds of 16 B per lane through a descriptor built from wave-uniform
+// inputs, made provably uniform (no waterfall loops around the loads); bytes == 0 drops every
+// lane (zeros land in LDS).  Kept out of the kernel template so the host pass never sees the
+// descriptor type.
+__device__ __forceinline__ void lean_load(const void* base, unsigned bytes, void* lds_dst, unsigned voff, unsigned soff) {
+    const unsigned long long b = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_dst, 16, voff, __builtin_amdgcn_readfirstlane(soff), 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN, int NW, int CG>
+__global__ __launch_bounds__(NW * 64) void igemm_x6_lean_kernel(const IgemmParams p) {
+    constexpr int FM = BM / WM / 32;
+    constexpr int FN = BN / WN / 32;
+    constexpr int A_LD = BM / (16 * NW);
+    constexpr int W_TOT = 6 * BN / 64;
+    constexpr int W_LD = (W_TOT + NW - 1) / NW;
+    constexpr bool SINK = (W_TOT % NW) != 0;
+    constexpr int G = A_LD + W_LD;
+    constexpr int A_FL = BM * 16;
+    constexpr int W_FL = BN * 6 * 4;
+    constexpr int STAGE = A_FL + W_FL;
+    constexpr int SPG = 9 * CG;               // stages per channel group (taps x 16-channel halves)
+    static_assert(WM * WN == NW && A_LD >= 1 && SPG % 3 == 0, "lean tile");
+
+    __shared__ __attribute__((aligned(16))) float lds[3 * STAGE + (SINK ? 256 : 0)];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int lr = lane & 31, lh = lane >> 5;
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kz = tile / (gridDim.x / p.ksplit);
+    tile -= kz * (gridDim.x / p.ksplit);
+    const int mb = tile / p.gn;
+    const int m_blk = mb * BM;
+    const int n_blk = (tile - mb * p.gn) * BN;
+
+    // pixel operand: shifted base so every in-image source offset is >= 0
+    const int cs = p.c0;                                      // == c1 when c1 != 0
+    const int shift = p.pad * p.Wi + p.pad;
+    const unsigned a_bytes0 = (unsigned)(((long long)p.in_pix + shift) * cs * 4);
+    const float* a0p = p.src0 - (long long)shift * cs;
+    const float* a1p = (p.c1 ? p.src1 : p.src0) - (long long)shift * cs;
+    const unsigned w_bytes = (unsigned)((long long)p.k_pad * p.N * 12);
+
+    const int lq = lane >> 2;
+    const int kc = (lane & 3) ^ ((lane >> 4) & 3);
+    unsigned vo[A_LD][9];
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) {
+        const int m = m_blk + wave * (BM / NW) + 16 * j + lq;
+        int hb = 0, wb = 0, pix = 0;
+        const bool mv = m < p.M;
+        if (mv) {
+            const int t = fdiv(m, p.dWo);
+            const int wo = m - t * p.Wo;
+            const int b = fdiv(t, p.dHo);
+            const int ho = t - b * p.Ho;
+            hb = ho * p.stride - p.pad;
+            wb = wo * p.stride - p.pad;
+            pix = (b * p.Hi + hb) * p.Wi + wb + shift;
+        }
+        const unsigned base = (unsigned)pix * (unsigned)(cs * 4) + kc * 16;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const bool ok = mv && (unsigned)(hb + r) < (unsigned)p.Hi && (unsigned)(wb + q) < (unsigned)p.Wi;
+                vo[j][r * 3 + q] = ok ? base : LEAN_OOB;
+            }
+    }
+    unsigned tapoff[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) tapoff[r * 3 + q] = (unsigned)((r * p.Wi + q) * cs * 4);
+    unsigned wv[W_LD];
+#pragma unroll
+    for (int j = 0; j < W_LD; ++j) {
+        const int I = wave + NW * j;
+        const int e = I * 64 + lane;
+        const int q = e / BN, row = e - q * BN;
+        const int n = n_blk + row;
+        wv[j] = (I < W_TOT && n < p.N) ? (unsigned)((q * p.N + n) * 16) : LEAN_OOB;
+    }
+    const unsigned w_stage = (unsigned)p.N * 96u;   // bytes of one 16-k stage's six planes
+
+    const int groups = p.k_pad / (16 * SPG);
+    const int gps = p.t_per / SPG;                  // groups per split
+    const int g0 = kz * gps;
+    const int g1 = min(groups, g0 + gps);
+
+    // loads of stage u (compile-time position in its group) of group g into ring slot u % 3
+    auto issue = [&](int g, auto uc) {
+        constexpr int u = decltype(uc)::value;
+        constexpr int tap = u / CG, h = u % CG;
+        const bool live = g < g1;
+        const int c = g * (16 * CG) + h * 16;                     // K-order channel of this stage
+        const bool second = c >= p.c0;
+        const float* abase = second ? a1p : a0p;
+        const unsigned abytes = live ? a_bytes0 : 0u;
+        const unsigned soff = tapoff[tap] + (unsigned)((second ? c - p.c0 : c) * 4);
+        float* a_slot = lds + (u % 3) * STAGE;
+#pragma unroll
+        for (int j = 0; j < A_LD; ++j)
+            lean_load(abase, abytes, a_slot + (wave * (BM / NW) + 16 * j) * 16, vo[j][tap], soff);
+        const unsigned wbytes = live ? w_bytes : 0u;
+        const unsigned wsoff = (unsigned)(g * SPG + u) * w_stage;
+        float* w_slot = a_slot + A_FL;
+#pragma unroll
+        for (int j = 0; j < W_LD; ++j) {
+            const int I = wave + NW * j;
+            float* dst = (!SINK || I < W_TOT) ? w_slot + I * 256 : lds + 3 * STAGE;
+            lean_load(p.wt, wbytes, dst, wv[j], wsoff);
+        }
+    };
+
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int a_row0 = wm * (BM / WM) + lr;
+    const int b_row0 = wn * (BN / WN) + lr;
+    const int swz = (lr >> 2) & 3;
+    const int pos0 = ((2 * lh) ^ swz) * 4, pos1 = ((2 * lh + 1) ^ swz) * 4;
+
+    if (g0 < g1) {
+        issue(g0, std::integral_constant<int, 0>{});
+        issue(g0, std::integral_constant<int, 1>{});
+    }
+    for (int g = g0; g < g1; ++g) {
+        static_for<SPG>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            __builtin_amdgcn_s_barrier();
+            const float* a = lds + (u % 3) * STAGE;
+            const float* wp = a + A_FL;
+            f32x4 xa[FM], xb[FM];
+            bf16x8_t fw[3][FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                xa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos0);
+                xb[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos1);
+            }
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int j = 0; j < FN; ++j)
+                    fw[pl][j] = *reinterpret_cast<const bf16x8_t*>(wp + ((pl * 2 + lh) * BN + b_row0 + j * 32) * 4);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+                bf16x8_t xh, xm, xl;
+                split3_pairs(xa[i], xb[i], xh, xm, xl);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) {
+                    f32x16 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xm, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[2][j], xh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xl, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xh, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xm, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xh, c, 0, 0, 0);
+                    acc[i][j] = c;
+                }
+                if (i == 0) {
+                    if constexpr (u + 2 < SPG) issue(g, std::integral_constant<int, u + 2>{});
+                    else issue(g + 1, std::integral_constant<int, u + 2 - SPG>{});
+                }
+            }
+        });
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (p.ksplit == 1) {
+        epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
+        return;
+    }
+    float* part = p.part + (long long)kz * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                if (n >= p.N) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                *reinterpret_cast<f32x4*>(part + (long long)m * p.N + n) = v;
+            }
+    }
+}
+
 // packed fp32 weight [n][k_pad] -> [k_pad/16][q][n][8] bf16 planes, q = plane*2 + (k%16)/8,
 // plane 0/1/2 = hi/mid/lo of the round-to-nearest split (exact: hi + mid + lo == w)
 __global__ void split_weight6_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int n, int k_pad) {
@@ -1148,6 +1407,20 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
                          // for N >= 256 (measured slower); 0 = 128x128 4-wave tiles everywhere
 #endif
 static bool uses_x6(const pu_conv_args* a);
+#ifndef PU_X6_LEAN
+#define PU_X6_LEAN 1     // igemm_x6_lean_kernel where it applies (0: igemm_x6_kernel everywhere)
+#endif
+static bool lean_ok(const pu_conv_args* a) {
+    if (!PU_X6_LEAN || !uses_x6(a)) return false;
+    const int C = a->c0 + a->c1;
+    if (a->kh != 3 || a->kw != 3 || !(a->cgroup == 16 || a->cgroup == 32)) return false;
+    if (a->c1 != 0 && a->c1 != a->c0) return false;
+    if (a->k_pad != 9 * C) return false;
+    const long long shift = (long long)a->pad * a->in_w + a->pad;
+    if (((long long)a->batch * a->in_h * a->in_w + shift) * a->c0 * 4 >= (1LL << 31)) return false;
+    if ((long long)a->k_pad * a->n * 12 >= (1LL << 31)) return false;
+    return true;
+}
 static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
     if (!(PU_X6_TILES && uses_x6(a))) {
         choose_tile(M, a->n, bm, bn);
@@ -1181,6 +1454,10 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
     if (ks > T / 8) ks = T / 8;
     if (ks < 2) return;
     *t_per = ceil_div(T, ks);
+    if (lean_ok(a)) {                  // the lean kernel splits K on channel-group boundaries
+        const int spg = 9 * (a->cgroup / 16);
+        *t_per = ceil_div(*t_per, spg) * spg;
+    }
     *ksplit = ceil_div(T, *t_per);
 }
 
@@ -1255,6 +1532,7 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     p.dTaps = make_fastdiv(p.taps);
     p.cgroup = a->cgroup;
     p.vec_epi = vec_epilogue(a);
+    p.in_pix = a->batch * a->in_h * a->in_w;
 
     const int mode = choose_mode(a->c0, a->c1);
     PU_REQUIRE(a->cgroup == 0 || a->cgroup == 16 || a->cgroup == 32, "pu_conv_igemm: cgroup %d", a->cgroup);
@@ -1291,6 +1569,29 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     if (a->weight6 && mode == LOAD_CHUNK16 && !PU_NO_DMA) {
         p.wt = reinterpret_cast<const float*>(a->weight6);
         PU_REQUIRE(((uintptr_t)a->weight6 & 15) == 0, "pu_conv_igemm: weight6 must be 16-byte aligned");
+        if (lean_ok(a)) {
+            const int cg = a->cgroup / 16;
+            bool done = true;
+#define PU_XL(BM_, BN_, WM_, WN_, NW_)                                                                          \
+    do {                                                                                                        \
+        if (cg == 2) hipLaunchKernelGGL((igemm_x6_lean_kernel<BM_, BN_, WM_, WN_, NW_, 2>), grid, dim3(NW_ * 64), 0, s, p); \
+        else hipLaunchKernelGGL((igemm_x6_lean_kernel<BM_, BN_, WM_, WN_, NW_, 1>), grid, dim3(NW_ * 64), 0, s, p); \
+    } while (0)
+            if (bm == 256 && bn == 128) PU_XL(256, 128, 8, 1, 8);
+            else if (bm == 256 && bn == 64) PU_XL(256, 64, 4, 1, 4);
+            else if (bm == 128 && bn == 128 && PU_X6_W41) PU_XL(128, 128, 4, 1, 4);
+            else if (bm == 128 && bn == 64 && !w41_64) PU_XL(128, 64, 2, 2, 4);
+            else if (bm == 64 && bn == 64) PU_XL(64, 64, 2, 2, 4);
+            else done = false;
+#undef PU_XL
+            if (done) {
+                if (p.ksplit > 1) {
+                    const long long tot = M * (N / 4);
+                    hipLaunchKernelGGL(igemm_splitk_epilogue_kernel, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s, p);
+                }
+                return check_launch("pu_conv_igemm (x6 lean)");
+            }
+        }
 #define PU_X6(BM_, BN_, WM_, WN_) hipLaunchKernelGGL((igemm_x6_kernel<BM_, BN_, WM_, WN_, PU_X6_NBUF, PU_X6_KSUB>), grid, dim3(256), 0, s, p)
         if (bm == 256 && bn == 256)
             hipLaunchKernelGGL((igemm_x6_kernel<256, 256, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
