@@ -241,18 +241,33 @@ __device__ __attribute__((aligned(16))) float g_wg_zero16[4] = {0.f, 0.f, 0.f, 0
 
 typedef __bf16 wg_bf16x8 __attribute__((ext_vector_type(8)));
 
-// 8 fp32 values -> their exact 3-term bf16 split (see igemm.hip, igemm_x6_kernel)
+// 8 fp32 values -> their exact 3-term bf16 split (see igemm.hip, igemm_x6_kernel), pair-wise:
+// v_cvt_pk_bf16_f32 rounds two values at once, the residuals are v_pk_add_f32 (4.5 VALU/element)
+typedef float wg_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 wg_bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned wg_pk(wg_f32x2 v) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(v, wg_bf16x2));
+}
 __device__ __forceinline__ void wg_split3(const float (&x)[8], wg_bf16x8& h, wg_bf16x8& m, wg_bf16x8& l) {
 #pragma clang fp contract(off)
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 hv, mv, lv;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const __bf16 a = (__bf16)x[e];
-        const float r = x[e] - (float)a;
-        const __bf16 b = (__bf16)r;
-        h[e] = a;
-        m[e] = b;
-        l[e] = (__bf16)(r - (float)b);
+    for (int q = 0; q < 4; ++q) {
+        const float x0 = x[2 * q], x1 = x[2 * q + 1];
+        const unsigned a = wg_pk(wg_f32x2{x0, x1});
+        const float r0 = x0 - __builtin_bit_cast(float, a << 16);
+        const float r1 = x1 - __builtin_bit_cast(float, a & 0xffff0000u);
+        const unsigned b = wg_pk(wg_f32x2{r0, r1});
+        const float l0 = r0 - __builtin_bit_cast(float, b << 16);
+        const float l1 = r1 - __builtin_bit_cast(float, b & 0xffff0000u);
+        hv[q] = a;
+        mv[q] = b;
+        lv[q] = wg_pk(wg_f32x2{l0, l1});
     }
+    h = __builtin_bit_cast(wg_bf16x8, hv);
+    m = __builtin_bit_cast(wg_bf16x8, mv);
+    l = __builtin_bit_cast(wg_bf16x8, lv);
 }
 
 // X6: the 16 staged pixel rows are one k-step of v_mfma_f32_32x32x16_bf16 and each fp32 product
@@ -512,6 +527,462 @@ __global__ __launch_bounds__(NW * 64) void wgrad_dma_kernel(const WgradParams p)
     }
 }
 
+typedef short wi16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) wi16x4 lds_i16x4_t;
+// swizzle of 16-byte chunks in 256-byte rows: conflict-free ds_read_b64_tr_b16
+__device__ __forceinline__ int wb_sw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// ------------------------------------------------ 6-product weight gradient over bf16 planes
+// The fp32 x6 kernel above splits every MFMA operand fragment in the wave that reads it, with
+// the fragment gathered by 8 strided ds_read_b32: ~12 issued instructions per MFMA on the
+// 128 x 256 tile (waves issue-bound, MFMA busy ~0.35).  Here the fp32 P / Q rows still arrive by
+// LDS-DMA, but each element is split ONCE per block: a split pass reads 4 consecutive fp32 of a
+// row (ds_read_b128), writes the hi / mid / lo bf16 quads (ds_write_b64) into row-major plane
+// images, and the MFMA operands come from those with ds_read_b64_tr_b16 (the transposed reads of
+// wgrad_bf16_kernel: 128-column images, 16-byte chunk ch of row r at ch ^ wb_sw(r)).  One barrier
+// per stage: the split pass of stage t+1 and the MFMAs of stage t share a phase (planes double
+// buffered).  Stride-1 same-size layers (FQ addressing), 8 waves.
+template <int BN, int BK, int WN, int WK, int NW>
+__global__ __launch_bounds__(NW * 64) void wgrad_x6p_kernel(const WgradParams p) {
+    constexpr int FN = BN / WN / 32;
+    constexpr int FK = BK / WK / 32;
+    constexpr int P_ROWS = 256 / BN;
+    constexpr int P_TOT = WG_BM / P_ROWS;
+    constexpr int P_LD = (P_TOT + NW - 1) / NW;
+    constexpr int Q_LD = WG_BM * BK / 256 / NW;
+    constexpr int G = P_LD + Q_LD;
+    constexpr int STAGE = WG_BM * (BN + BK);              // fp32 ring slot (floats)
+    constexpr int SINK = (P_TOT % NW) ? 256 : 0;
+    constexpr int NIMG = BN / 128 + BK / 128;            // 128-column plane images per plane
+    constexpr int IMGB = WG_BM * 256;                     // bytes of one image (16 rows x 256 B)
+    constexpr int PLANES = 3 * NIMG * IMGB;               // bytes of one plane buffer (3 planes)
+    constexpr int GROUPS = WG_BM * (BN + BK) / 4;         // float4 groups per stage
+    constexpr int GPT = (GROUPS + NW * 64 - 1) / (NW * 64);
+    static_assert(WN * WK == NW && P_LD >= 1 && Q_LD >= 1 && BN % 128 == 0 && BK % 128 == 0 && FN >= 1 && FK >= 1,
+                  "x6p tile");
+
+    __shared__ __attribute__((aligned(16))) float lds[3 * STAGE + SINK + 2 * PLANES / 4];
+    char* const planes = reinterpret_cast<char*>(lds + 3 * STAGE + SINK);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave % WN, wk = wave / WN;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % p.gx;
+    const int tyz = tile / p.gx;
+    const int ty = tyz % p.gy;
+    const int tz = tyz / p.gy;
+    const int n_blk = ty * BN;
+    const int k_blk = tx * BK;
+    const int m_begin = tz * p.mps;
+    const int m_end = min(p.M, m_begin + p.mps);
+
+    // ---- loader geometry (as wgrad_dma_kernel, FQ addressing)
+    const int p_col = (lane % (BN / 4)) * 4;
+    const int p_dr = lane / (BN / 4);
+    const int pn = n_blk + p_col;
+    const bool p_in = pn < p.N;
+    const float* p_lane = p.P + (long long)p_dr * p.N + pn;
+    // per Q piece j: lane row delta, tap offsets, source stride (0: k past K -> zero page) and
+    // the lane's source pointer at m = 0 (host guarantees every source under 2^31 elements, so
+    // the per-stage offset m * cs is one 24-bit multiply)
+    int q_dr[Q_LD], q_r[Q_LD], q_s[Q_LD], q_row0[Q_LD], q_cs[Q_LD];
+    const float* q_fb[Q_LD];
+#pragma unroll
+    for (int j = 0; j < Q_LD; ++j) {
+        const int base = (wave * Q_LD + j) * 256;
+        const int off = base + 4 * lane;
+        q_row0[j] = base / BK;
+        q_dr[j] = off / BK - q_row0[j];
+        const int qk = min(k_blk + off % BK, p.K - 1);
+        const int tap = fdiv(qk, p.dC);
+        const int c = qk - tap * p.C;
+        const int r = fdiv(tap, p.dKw);
+        const int sq = tap - r * p.kw;
+        const bool first = c < p.c0;
+        const int cs = first ? p.c0 : p.c1;
+        const float* q_ptr = first ? p.src0 + c : p.src1 + (c - p.c0);
+        q_fb[j] = q_ptr + (long long)(q_dr[j] + (r - p.pad) * p.Wi + (sq - p.pad)) * cs;
+        q_cs[j] = (k_blk + off % BK < p.K) ? cs : 0;
+        q_r[j] = r - p.pad;
+        q_s[j] = sq - p.pad;
+    }
+
+    auto issue = [&](int m0, int slot) {
+        float* ps = lds + slot * STAGE;
+        float* qs = ps + WG_BM * BN;
+#pragma unroll
+        for (int j = 0; j < P_LD; ++j) {
+            const int I = (P_TOT % NW) ? wave + NW * j : wave * P_LD + j;
+            const int row0 = I * P_ROWS;
+            const int m = m0 + row0 + p_dr;
+            const float* g = g_wg_zero16;
+            float* dst = ps + row0 * BN;
+            if (SINK && I >= P_TOT) dst = lds + 3 * STAGE;
+            else if (m < m_end && p_in) g = p_lane + (long long)(m0 + row0) * p.N;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)dst, 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < Q_LD; ++j) {
+            const int mu = m0 + q_row0[j];
+            const int tu = fdiv(mu, p.dWo);
+            const int wou = mu - tu * p.Wo;
+            const int bu = fdiv(tu, p.dHo);
+            const int hou = tu - bu * p.Ho;
+            int wo = wou + q_dr[j];
+            const bool cw = wo >= p.Wo;
+            wo = cw ? wo - p.Wo : wo;
+            int ho = hou + (cw ? 1 : 0);
+            ho = ho >= p.Ho ? ho - p.Ho : ho;
+            const int hi = ho + q_r[j], wi = wo + q_s[j];
+            const bool ok = mu + q_dr[j] < m_end && q_cs[j] != 0 && (unsigned)hi < (unsigned)p.Hi &&
+                            (unsigned)wi < (unsigned)p.Wi;
+            const float* g = ok ? q_fb[j] + __umul24((unsigned)mu, (unsigned)q_cs[j]) : g_wg_zero16;
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(qs + (wave * Q_LD + j) * 256), 16, 0, 0);
+        }
+    };
+
+    // ---- split pass: fp32 slot -> plane buffer (row-major 128-column images, swizzled chunks)
+    auto img_off = [](int row, int col) {   // byte offset of (row, col) within one image
+        return row * 256 + 16 * ((col >> 3) ^ wb_sw(row)) + 2 * (col & 7);
+    };
+    auto split_pass = [&](int slot, int buf) {
+        const float* src = lds + slot * STAGE;
+        char* pb = planes + buf * PLANES;
+#pragma unroll
+        for (int i = 0; i < GPT; ++i) {
+            const int g = tid + i * NW * 64;
+            if (GROUPS % (NW * 64) != 0 && g >= GROUPS) break;
+            const bool isp = g < WG_BM * BN / 4;
+            const int gg = isp ? g : g - WG_BM * BN / 4;
+            const int w4 = (isp ? BN : BK) / 4;
+            const int row = gg / w4;
+            const int col = (gg - row * w4) * 4;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(src + (isp ? 0 : WG_BM * BN) + row * (isp ? BN : BK) + col);
+            const int img = isp ? (col >> 7) : BN / 128 + (col >> 7);
+            unsigned h[2], m[2], l[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+#pragma clang fp contract(off)
+                const float x0 = v[2 * q], x1 = v[2 * q + 1];
+                const unsigned a = wg_pk(wg_f32x2{x0, x1});
+                const float r0 = x0 - __builtin_bit_cast(float, a << 16);
+                const float r1 = x1 - __builtin_bit_cast(float, a & 0xffff0000u);
+                const unsigned b = wg_pk(wg_f32x2{r0, r1});
+                const float l0 = r0 - __builtin_bit_cast(float, b << 16);
+                const float l1 = r1 - __builtin_bit_cast(float, b & 0xffff0000u);
+                h[q] = a;
+                m[q] = b;
+                l[q] = wg_pk(wg_f32x2{l0, l1});
+            }
+            char* dst = pb + img * IMGB + img_off(row, col & 127);
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<u32x2*>(dst) = u32x2{h[0], h[1]};
+            *reinterpret_cast<u32x2*>(dst + NIMG * IMGB) = u32x2{m[0], m[1]};
+            *reinterpret_cast<u32x2*>(dst + 2 * NIMG * IMGB) = u32x2{l[0], l[1]};
+        }
+    };
+
+    f32x16 acc[FK][FN];
+#pragma unroll
+    for (int i = 0; i < FK; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // transposed reads (wgrad_bf16_kernel): 16-lane group grp covers columns 16*(grp&1) + 0..15
+    // and rows 8*(grp>>1) + (0..3 | 4..7); lane 4q+p of a group addresses row q, columns 4p..4p+3
+    const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
+    const int row0 = 8 * (grp >> 1) + gq;
+    const int ccol = 16 * (grp & 1) + 4 * gp;
+    auto frag = [&](const char* pb, int pl, int col) {   // col: first plane column of the fragment
+        const char* base = pb + (pl * NIMG + (col >> 7)) * IMGB;
+        const int c = (col & 127) + ccol;
+        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(base + img_off(row0, c)));
+        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(base + img_off(row0 + 4, c)));
+        typedef short wi16x8 __attribute__((ext_vector_type(8)));
+        const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        return __builtin_bit_cast(wg_bf16x8, av);
+    };
+
+    const int T = (m_end > m_begin) ? (m_end - m_begin + WG_BM - 1) / WG_BM : 0;
+    const int bias_w = (p.bias_mode == 1 && tx == 0) ? BN : (p.bias_mode == 2 && ty == 0) ? BK : 0;
+    float bsum = 0.f;
+    auto bias_sum = [&](int slot) {
+        if (tid < bias_w) {
+            const float* img = lds + slot * STAGE + (p.bias_mode == 1 ? 0 : WG_BM * BN);
+#pragma unroll
+            for (int r = 0; r < WG_BM; ++r) bsum += img[r * bias_w + tid];
+        }
+    };
+
+    issue(m_begin, 0);
+    issue(m_begin + WG_BM, 1);
+    issue(m_begin + 2 * WG_BM, 2);
+    if (T > 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+        __builtin_amdgcn_s_barrier();
+        split_pass(0, 0);
+        bias_sum(0);
+    }
+    for (int t = 0; t < T; ++t) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");   // stage t+1 landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         // my plane writes / reads done
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        issue(m_begin + (t + 3) * WG_BM, t % 3);
+        if (t + 1 < T) {
+            split_pass((t + 1) % 3, (t + 1) & 1);
+            bias_sum((t + 1) % 3);
+        }
+        const char* pb = planes + (t & 1) * PLANES;
+        wg_bf16x8 ph[FN], pm[FN], pl[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int col = wn * (BN / WN) + j * 32;
+            ph[j] = frag(pb, 0, col);
+            pm[j] = frag(pb, 1, col);
+            pl[j] = frag(pb, 2, col);
+        }
+#pragma unroll
+        for (int i = 0; i < FK; ++i) {
+            const int col = BN + wk * (BK / WK) + i * 32;
+            const wg_bf16x8 qh = frag(pb, 0, col), qm = frag(pb, 1, col), ql = frag(pb, 2, col);
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+                f32x16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm[j], c, 0, 0, 0);   // small terms first
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph[j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pl[j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, ph[j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pm[j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph[j], c, 0, 0, 0);
+                acc[i][j] = c;
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
+    if (tid < bias_w) {
+        if (p.bias_mode == 1) {
+            const int n = n_blk + tid;
+            if (n < p.N) slab[(long long)n * p.Kcp + p.K] = bsum;
+        } else {
+            const int k = k_blk + tid;
+            if (k < p.K) slab[(long long)p.N * p.Kcp + k] = bsum;
+        }
+    }
+    const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int n = n_blk + wn * (BN / WN) + j * 32 + lr;
+        if (n >= p.N) continue;
+#pragma unroll
+        for (int i = 0; i < FK; ++i) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = k_blk + wk * (BK / WK) + i * 32 + 8 * q + 4 * lh;
+                if (k >= p.K) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
+            }
+        }
+    }
+}
+
+// ------------------------------------------ 6-product weight gradient with halo reuse (3x3/s1)
+// dW[n][tap][c] = sum_m dZ[m][n] * X[m + tap][c].  A stage is 16 consecutive output pixels of one
+// image row; the 9 taps read only the 3 x 18 halo pixels around them, so the block loads and
+// splits that halo ONCE (54 pixel rows x 64 channels, instead of 9 x 16 im2col rows) together
+// with the 16 dZ rows (64 channels), writes the hi / mid / lo bf16 planes into LDS (row-major,
+// 128-byte rows, 16-byte chunk ch of row r at ch ^ 4*((r >> 1) & 1): conflict-free transposed
+// reads), and every wave reads its MFMA operands with ds_read_b64_tr_b16: tap (r, s) is the
+// 16-row window starting at halo row 18 r + s.  Block tile: 64 output channels x 64 input
+// channels x all 9 taps, 4 waves = (channel half, output half), each 9 accumulators (one per
+// tap).  Raw fp32 rows arrive in registers one stage ahead (global_load_dwordx4; halo pixels
+// outside the image are zero); the planes are double buffered, one barrier per stage.
+// Requires stride 1, pad 1, 3x3, Hi == Ho, Wi == Wo, Wo % 16 == 0, c0 % 64 == c1 % 64 == 0,
+// N % 64 == 0, bias_mode != 2, every source under 2^31 elements.
+constexpr int HX_ROWS = 54;                   // halo pixel rows (3 x 18)
+constexpr int HX_IMG = (HX_ROWS + 16) * 128;  // bytes of one plane: X rows, then 16 dZ rows
+__device__ __forceinline__ int hx_off(int row, int col) {   // byte offset in a 64-column plane
+    return row * 128 + 16 * ((col >> 3) ^ (((row >> 1) & 1) << 2)) + 2 * (col & 7);
+}
+
+__global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p) {
+    constexpr int XG = 4;                     // X float4 groups per thread (864 = 3 x 256 + 96)
+    __shared__ __attribute__((aligned(16))) char lds[2 * 3 * HX_IMG];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ci = wave & 1, nj = wave >> 1;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % p.gx;               // 64-channel input tile
+    const int tyz = tile / p.gx;
+    const int ty = tyz % p.gy;                // 64-channel output tile
+    const int tz = tyz / p.gy;
+    const int m_begin = tz * p.mps;
+    const int m_end = min(p.M, m_begin + p.mps);
+    const int T = m_end > m_begin ? (m_end - m_begin) / 16 : 0;
+
+    // ---- thread roles in the loads: column quad cq (fixed), halo pixel rows hp_i = tid/16 + 16 i
+    const int cq = tid & 15;
+    const int c_lo = tx * 64;                 // first input channel of the tile
+    const bool first = c_lo < p.c0;
+    const float* xsrc = first ? p.src0 + c_lo : p.src1 + (c_lo - p.c0);
+    const int cs = first ? p.c0 : p.c1;
+    const float* x_lane[XG];
+    unsigned x_cls[XG];                       // edge classes: 1 top, 2 bottom, 4 left, 8 right, 16 none
+#pragma unroll
+    for (int i = 0; i < XG; ++i) {
+        const int hp = (tid >> 4) + 16 * i;
+        const int rr = hp / 18, cc = hp - rr * 18;
+        x_lane[i] = xsrc + (long long)((rr - 1) * p.Wi + (cc - 1)) * cs + cq * 4;
+        x_cls[i] = hp >= HX_ROWS ? 0u
+                                 : ((rr == 0 ? 1u : 0u) | (rr == 2 ? 2u : 0u) | (cc == 0 ? 4u : 0u) | (cc == 17 ? 8u : 0u));
+    }
+    const float* p_lane = p.P + (long long)(tid >> 4) * p.N + ty * 64 + cq * 4;
+
+    f32x4 rx[XG], rp;
+    auto load = [&](int t) {                  // raw rows of stage t into registers
+        const int m0 = m_begin + 16 * t;
+        const int tu = fdiv(m0, p.dWo);
+        const int wo0 = m0 - tu * p.Wo;
+        const int bu = fdiv(tu, p.dHo);
+        const int ho = tu - bu * p.Ho;
+        const unsigned flags = (ho == 0 ? 1u : 0u) | (ho == p.Ho - 1 ? 2u : 0u) | (wo0 == 0 ? 4u : 0u) |
+                               (wo0 + 16 == p.Wo ? 8u : 0u);
+        const bool live = t < T;
+#pragma unroll
+        for (int i = 0; i < XG; ++i) {
+            const bool row = i < 3 || (tid >> 4) + 48 < HX_ROWS;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (row && live && !(x_cls[i] & flags)) v = *reinterpret_cast<const f32x4*>(x_lane[i] + (long long)m0 * cs);
+            rx[i] = v;
+        }
+        rp = live ? *reinterpret_cast<const f32x4*>(p_lane + (long long)m0 * p.N) : f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
+    const bool bias_blk = p.bias_mode == 1 && tx == 0;
+    auto split_store = [&](int buf) {         // registers -> bf16 planes of buffer buf
+        char* pb = lds + buf * 3 * HX_IMG;
+        auto put = [&](int row, const f32x4 v) {
+            unsigned h[2], m[2], l[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+#pragma clang fp contract(off)
+                const float x0 = v[2 * q], x1 = v[2 * q + 1];
+                const unsigned a = wg_pk(wg_f32x2{x0, x1});
+                const float r0 = x0 - __builtin_bit_cast(float, a << 16);
+                const float r1 = x1 - __builtin_bit_cast(float, a & 0xffff0000u);
+                const unsigned b = wg_pk(wg_f32x2{r0, r1});
+                const float l0 = r0 - __builtin_bit_cast(float, b << 16);
+                const float l1 = r1 - __builtin_bit_cast(float, b & 0xffff0000u);
+                h[q] = a;
+                m[q] = b;
+                l[q] = wg_pk(wg_f32x2{l0, l1});
+            }
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            char* dst = pb + hx_off(row, cq * 4);
+            *reinterpret_cast<u32x2*>(dst) = u32x2{h[0], h[1]};
+            *reinterpret_cast<u32x2*>(dst + HX_IMG) = u32x2{m[0], m[1]};
+            *reinterpret_cast<u32x2*>(dst + 2 * HX_IMG) = u32x2{l[0], l[1]};
+        };
+#pragma unroll
+        for (int i = 0; i < XG; ++i) {
+            const int hp = (tid >> 4) + 16 * i;
+            if (i < 3 || hp < HX_ROWS) put(hp, rx[i]);
+        }
+        put(HX_ROWS + (tid >> 4), rp);
+        if (bias_blk) bsum += rp;
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t9][r] = 0.f;
+
+    // transposed reads: group grp = lane>>4 covers columns 16 (grp&1) + 0..15, rows 8 (grp>>1) +
+    // gq (+4); lane 4 gq + gp addresses row gq, columns 4 gp .. 4 gp + 3
+    const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
+    const int rsub = 8 * (grp >> 1) + gq;
+    const int ccol = 16 * (grp & 1) + 4 * gp;
+    auto frag = [&](const char* plane, int row0, int col0) {
+        const int row = row0 + rsub, col = col0 + ccol;
+        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(plane + hx_off(row, col)));
+        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(plane + hx_off(row + 4, col)));
+        typedef short wi16x8 __attribute__((ext_vector_type(8)));
+        const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        return __builtin_bit_cast(wg_bf16x8, av);
+    };
+
+    if (T > 0) {
+        load(0);
+        split_store(0);
+        load(1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    for (int t = 0; t < T; ++t) {
+        const char* pb = lds + (t & 1) * 3 * HX_IMG;
+        const wg_bf16x8 ph = frag(pb, HX_ROWS, nj * 32), pm = frag(pb + HX_IMG, HX_ROWS, nj * 32),
+                        pl = frag(pb + 2 * HX_IMG, HX_ROWS, nj * 32);
+#pragma unroll
+        for (int t9 = 0; t9 < 9; ++t9) {
+            const int row0 = (t9 / 3) * 18 + (t9 % 3);
+            const wg_bf16x8 qh = frag(pb, row0, ci * 32), qm = frag(pb + HX_IMG, row0, ci * 32),
+                            ql = frag(pb + 2 * HX_IMG, row0, ci * 32);
+            f32x16 c = acc[t9];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm, c, 0, 0, 0);   // small terms first
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pl, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, ph, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pm, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph, c, 0, 0, 0);
+            acc[t9] = c;
+        }
+        if (t + 1 < T) {
+            split_store((t + 1) & 1);         // raw(t+1) has been in flight for a whole stage
+            load(t + 2);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+
+    float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
+    if (bias_blk) {                           // column sums of dZ: 16 rows of partials per column
+        f32x4* red = reinterpret_cast<f32x4*>(lds);
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < 16) {
+            f32x4 v = red[tid];
+            for (int r = 1; r < 16; ++r) v += red[r * 16 + tid];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) slab[(long long)(ty * 64 + tid * 4 + e) * p.Kcp + p.K] = v[e];
+        }
+    }
+    const int lr = lane & 31, lh = lane >> 5;
+    const int n = ty * 64 + nj * 32 + lr;
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = t9 * p.C + c_lo + ci * 32 + 8 * q + 4 * lh;
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[t9][4 * q + e];
+            *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
+        }
+    }
+}
+
 // ------------------------------------------------------------- small-channel weight gradient
 // 3x3/s1/p1 with C <= 16 input and N <= 16 output channels (configs C4/C5's 8/16-channel levels):
 // a GEMM with N, K this small wastes most of an MFMA tile, so each block sweeps 16 x 32 pixel
@@ -709,7 +1180,7 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
 
 struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
-    bool qvec, dma, small;
+    bool qvec, dma, small, x6p, halo;
     int tiles_w, tiles_h;
     size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
     size_t part_bytes() const { return G > 1 ? (size_t)G * Nr * Kcp * sizeof(double) : 0; }
@@ -737,6 +1208,12 @@ static bool small_wgrad_ok(const pu_wgrad_args* a) {
 #ifndef PU_WG_FQ
 #define PU_WG_FQ 1         // stride-1 same-size layers: scalar + compare-and-wrap Q addressing
 #endif
+#ifndef PU_WG_HALO
+#define PU_WG_HALO 1       // 3x3/s1 layers with 64-channel multiples: halo-reuse kernel (wgrad_halo_x6_kernel)
+#endif
+#ifndef PU_WG_X6P
+#define PU_WG_X6P 0        // N >= 128 stride-1 layers: split-once bf16 planes kernel (wgrad_x6p_kernel)
+#endif
 #ifndef PU_WG_X6_W3
 #define PU_WG_X6_W3 0      // 6-product 64-channel layers with K % 192 == 0 on 64 x 192 tiles as 3 waves of 64 x 64
 #endif
@@ -761,6 +1238,8 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->Kcp = (pl->Kc + 3) / 4 * 4;
     pl->qvec = (a->c0 % 4 == 0) && (a->c1 % 4 == 0);
     pl->small = small_wgrad_ok(a);
+    pl->x6p = false;
+    pl->halo = false;
     if (pl->qvec) {
         PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0, "pu_wgrad: sources must be 16-byte aligned");
     }
@@ -808,6 +1287,37 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
         pl->BK = 576;
         occ = PU_WG_W6_NBUF == 3 ? 1 : 2;
     }
+    pl->x6p = false;
+    pl->halo = false;
+    if (PU_WG_HALO && a->math == 1 && pl->dma && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
+        a->in_h == a->out_h && a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 &&
+        a->n % 64 == 0 && a->bias_mode != 2 && (long long)a->batch * a->in_h * a->in_w * (pl->C) < (1LL << 31)) {
+        pl->halo = true;
+        pl->BN = 64;
+        pl->BK = 9 * 64;
+        const int tiles = (pl->C / 64) * (a->n / 64);
+        int splits = 512 / tiles;                     // two 4-wave blocks per CU
+        const int stages = (int)(M / 16);
+        if (splits > stages) splits = stages;
+        if (splits < 1) splits = 1;
+        pl->mps = ceil_div(stages, splits) * 16;
+        pl->splits = ceil_div((int)M, pl->mps);
+        pl->gx = pl->C / 64;
+        pl->gy = a->n / 64;
+        const long long total = (long long)pl->Nr * pl->Kcp;
+        int G = (int)ceil_div(262144LL, total);
+        const int by_len = ceil_div(pl->splits, 8);
+        if (G > by_len) G = by_len;
+        if (G > 16) G = 16;
+        pl->G = G < 1 ? 1 : G;
+        return PU_OK;
+    }
+    if (PU_WG_X6P && a->math == 1 && pl->dma && pl->BN == 128 && a->stride == 1 && a->in_h == a->out_h &&
+        a->in_w == a->out_w && a->out_w >= 4) {
+        pl->BK = 256;      // wgrad_x6p_kernel<128, 256, 2, 4, 8>: one 8-wave block per CU (144 KB of LDS)
+        pl->x6p = true;
+        occ = 1;
+    }
     if (PU_WG_X6_W3 && a->math == 1 && pl->dma && pl->BN == 64 && ext_k % 192 == 0) {
         pl->BK = -192;   // marker: the 3-wave kernel (tile width 192)
         occ = 4;
@@ -848,14 +1358,11 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
 // sw(r) = ((r&3)<<2) | ((r>>2)&3) (conflict-free transposed reads on 256-byte rows); glds cannot
 // permute its LDS writes, so each lane fetches the global chunk that belongs at its position.
 typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
-typedef short wi16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) wi16x4 lds_i16x4_t;
 __device__ __attribute__((aligned(16))) __bf16 g_wg_zero_b16[8];
 
 constexpr int WB_ROWS = 32;   // pixel rows per stage (2 MFMA k-steps)
 constexpr int WB_W = 128;     // columns per image (BN = BK = 128)
 
-__device__ __forceinline__ int wb_sw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
 struct WgradBf16Params {
     int M, N, K, Kcp, Nr, C, c0, c1;
@@ -1128,7 +1635,7 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
     if (st != PU_OK) return st;
     if (bn) *bn = pl.BN;
     if (bk) *bk = pl.BK < 0 ? -pl.BK : pl.BK;
-    if (qvec) *qvec = pl.small ? 2 : (pl.qvec ? 1 : 0);   // 2: small-channel direct kernel
+    if (qvec) *qvec = pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo kernel
     if (splits) *splits = pl.splits;
     return PU_OK;
 }
@@ -1181,7 +1688,11 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
         else hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, false>), grid, dim3(256), 0, s, p); \
     } while (0)
 #define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
-        if (pl.dma) {
+        if (pl.halo) {
+            hipLaunchKernelGGL(wgrad_halo_x6_kernel, grid, dim3(256), 0, s, p);
+        } else if (pl.x6p) {
+            hipLaunchKernelGGL((wgrad_x6p_kernel<128, 256, 2, 4, 8>), grid, dim3(512), 0, s, p);
+        } else if (pl.dma) {
             if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
             else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
             else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);

@@ -240,8 +240,8 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct")[qv.value])
-    if a.math == 1 and qv.value == 1:
+    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct", "halo")[qv.value])
+    if a.math == 1 and qv.value in (1, 3):
         tag = tag[:-1] + ",x6>"
     # the GEMM and the split reduction timed apart (they are separate kernels in rocprof too)
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):

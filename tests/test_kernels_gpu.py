@@ -52,6 +52,10 @@ CONV_CASES = [
     (2, 8, 8, 48, 0, 64),       # wgrad 64x128 tile, ragged last k-tile, bias column sums
     (1, 8, 8, 64, 64, 32),      # wgrad 64x128 tile, two sources
     (2, 9, 13, 64, 64, 64),     # wgrad 64x576 6-wave tile (K = 2 x 576), two sources, ragged pixels
+    (2, 12, 20, 128, 128, 256), # wgrad split-once planes kernel (128x256): two sources, non-square
+    (1, 9, 13, 64, 0, 136),     # planes kernel: N not a tile multiple, ragged pixels, ragged k-tile
+    (2, 16, 32, 64, 64, 128),   # halo-reuse wgrad: two sources, 2 x 2 channel tiles, image-row edges
+    (1, 32, 16, 192, 0, 64),    # halo-reuse wgrad: 3 input-channel tiles, 16-wide rows (every stage at both edges)
     (2, 37, 45, 16, 0, 16),     # small-channel direct kernels: several 16x32 tiles, ragged edges
     (1, 19, 70, 4, 4, 4),       # small-channel, two 4-channel sources, N = 4
 ]
