@@ -18,7 +18,12 @@ import sys
 
 
 def tag_of(name):
-    m = re.search(r"wgrad_dma_kernel<(\d+), (\d+), \d+, \d+, \d+, (true|false)>", name)
+    if "wgrad_halo_x6_kernel" in name:
+        return "wgrad<64x576,halo,x6>"
+    m = re.search(r"igemm_x6_lean_kernel<(\d+), (\d+),", name)
+    if m:
+        return "igemm<%sx%s,x6>" % m.groups()
+    m = re.search(r"wgrad_dma_kernel<(\d+), (\d+), \d+, \d+, \d+, (true|false)[,>]", name)
     if m:
         return "wgrad<%sx%s,vec4%s>" % (m.group(1), m.group(2), ",x6" if m.group(3) == "true" else "")
     m = re.search(r"igemm_x6_kernel<(\d+), (\d+),", name)
