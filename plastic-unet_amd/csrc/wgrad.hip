@@ -12,6 +12,7 @@
 // Partial tiles go to a per-split slab; wgrad_reduce sums the splits in a fixed order
 // (deterministic) and writes PyTorch's [n][c][kh][kw] layout.
 #include "common.h"
+#include <type_traits>
 
 namespace pu {
 
@@ -838,41 +839,48 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     const float* xsrc = first ? p.src0 + c_lo : p.src1 + (c_lo - p.c0);
     const int cs = first ? p.c0 : p.c1;
     const float* x_lane[XG];
-    unsigned x_cls[XG];                       // edge classes: 1 top, 2 bottom, 4 left, 8 right, 16 none
+    unsigned x_cls[XG];                       // edge classes: 1 top, 2 bottom, 4 left, 8 right, 16 past the halo, 32 all
 #pragma unroll
     for (int i = 0; i < XG; ++i) {
         const int hp = (tid >> 4) + 16 * i;
         const int rr = hp / 18, cc = hp - rr * 18;
         x_lane[i] = xsrc + (long long)((rr - 1) * p.Wi + (cc - 1)) * cs + cq * 4;
-        x_cls[i] = hp >= HX_ROWS ? 0u
-                                 : ((rr == 0 ? 1u : 0u) | (rr == 2 ? 2u : 0u) | (cc == 0 ? 4u : 0u) | (cc == 17 ? 8u : 0u));
+        if (hp >= HX_ROWS) x_lane[i] = g_wg_zero16;   // rows past the halo: class 16 -> zero page, never stored
+        x_cls[i] = 32u | (hp >= HX_ROWS ? 16u
+                                        : ((rr == 0 ? 1u : 0u) | (rr == 2 ? 2u : 0u) | (cc == 0 ? 4u : 0u) | (cc == 17 ? 8u : 0u)));
     }
     const float* p_lane = p.P + (long long)(tid >> 4) * p.N + ty * 64 + cq * 4;
 
     f32x4 rx[XG], rp;
-    auto load = [&](int t) {                  // raw rows of stage t into registers
-        const int m0 = m_begin + 16 * t;
+    auto load = [&](int t) {                  // raw rows of stage t into registers (branch-free:
+        const int m0 = m_begin + 16 * t;      // out-of-image halo pixels read the zero page)
         const int tu = fdiv(m0, p.dWo);
         const int wo0 = m0 - tu * p.Wo;
         const int bu = fdiv(tu, p.dHo);
         const int ho = tu - bu * p.Ho;
-        const unsigned flags = (ho == 0 ? 1u : 0u) | (ho == p.Ho - 1 ? 2u : 0u) | (wo0 == 0 ? 4u : 0u) |
-                               (wo0 + 16 == p.Wo ? 8u : 0u);
         const bool live = t < T;
+        // a stage past the split's end (prefetch beyond T) reads the zero page in every lane
+        const unsigned flags = live ? (16u | (ho == 0 ? 1u : 0u) | (ho == p.Ho - 1 ? 2u : 0u) | (wo0 == 0 ? 4u : 0u) |
+                                       (wo0 + 16 == p.Wo ? 8u : 0u))
+                                    : 0xffffffffu;
+        const unsigned xo = __umul24((unsigned)m0, (unsigned)cs);
 #pragma unroll
         for (int i = 0; i < XG; ++i) {
-            const bool row = i < 3 || (tid >> 4) + 48 < HX_ROWS;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (row && live && !(x_cls[i] & flags)) v = *reinterpret_cast<const f32x4*>(x_lane[i] + (long long)m0 * cs);
-            rx[i] = v;
+            const float* g = (x_cls[i] & flags) ? g_wg_zero16 : x_lane[i] + xo;
+            rx[i] = *reinterpret_cast<const f32x4*>(g);
         }
-        rp = live ? *reinterpret_cast<const f32x4*>(p_lane + (long long)m0 * p.N) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* gp = live ? p_lane + __umul24((unsigned)m0, (unsigned)p.N) : g_wg_zero16;
+        rp = *reinterpret_cast<const f32x4*>(gp);
     };
     f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
     const bool bias_blk = p.bias_mode == 1 && tx == 0;
+    // plane writes: halo rows hp_i = hp_0 + 16 i keep the swizzle of hp_0 (16 i = 0 mod 4), so
+    // every write of a thread is one base address plus an immediate
+    const int w_base = hx_off(tid >> 4, cq * 4);
+    const int wp_base = hx_off(HX_ROWS + (tid >> 4), cq * 4);
     auto split_store = [&](int buf) {         // registers -> bf16 planes of buffer buf
         char* pb = lds + buf * 3 * HX_IMG;
-        auto put = [&](int row, const f32x4 v) {
+        auto put = [&](char* dst, const f32x4 v) {
             unsigned h[2], m[2], l[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
@@ -889,7 +897,6 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
                 l[q] = wg_pk(wg_f32x2{l0, l1});
             }
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            char* dst = pb + hx_off(row, cq * 4);
             *reinterpret_cast<u32x2*>(dst) = u32x2{h[0], h[1]};
             *reinterpret_cast<u32x2*>(dst + HX_IMG) = u32x2{m[0], m[1]};
             *reinterpret_cast<u32x2*>(dst + 2 * HX_IMG) = u32x2{l[0], l[1]};
@@ -897,9 +904,9 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
 #pragma unroll
         for (int i = 0; i < XG; ++i) {
             const int hp = (tid >> 4) + 16 * i;
-            if (i < 3 || hp < HX_ROWS) put(hp, rx[i]);
+            if (i < 3 || hp < HX_ROWS) put(pb + w_base + i * 16 * 128, rx[i]);
         }
-        put(HX_ROWS + (tid >> 4), rp);
+        put(pb + wp_base, rp);
         if (bias_blk) bsum += rp;
     };
 
@@ -914,31 +921,28 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
     const int rsub = 8 * (grp >> 1) + gq;
     const int ccol = 16 * (grp & 1) + 4 * gp;
-    auto frag = [&](const char* plane, int row0, int col0) {
-        const int row = row0 + rsub, col = col0 + ccol;
-        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(plane + hx_off(row, col)));
-        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(plane + hx_off(row + 4, col)));
+    // tap (r, s) reads halo rows 18 r + s + rsub (+4): rows congruent mod 4 share the swizzle, so
+    // the 9 taps need 3 base addresses (18 r + s mod 4 in {0, 1, 2, 3}) plus immediates
+    int xb[4];
+#pragma unroll
+    for (int res = 0; res < 4; ++res) xb[res] = hx_off(res + rsub, ci * 32 + ccol);
+    const int pbase = hx_off(HX_ROWS + rsub, nj * 32 + ccol);
+    auto tr2 = [&](const char* a) {           // rows +0 / +4 of a fragment -> one MFMA operand
+        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a);
+        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a + 4 * 128));
         typedef short wi16x8 __attribute__((ext_vector_type(8)));
         const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
         return __builtin_bit_cast(wg_bf16x8, av);
     };
-
-    if (T > 0) {
-        load(0);
-        split_store(0);
-        load(1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    }
-    for (int t = 0; t < T; ++t) {
-        const char* pb = lds + (t & 1) * 3 * HX_IMG;
-        const wg_bf16x8 ph = frag(pb, HX_ROWS, nj * 32), pm = frag(pb + HX_IMG, HX_ROWS, nj * 32),
-                        pl = frag(pb + 2 * HX_IMG, HX_ROWS, nj * 32);
+    auto mfma_stage = [&](auto bufc) {
+        constexpr int buf = decltype(bufc)::value;
+        const char* pb = lds + buf * 3 * HX_IMG;
+        const wg_bf16x8 ph = tr2(pb + pbase), pm = tr2(pb + HX_IMG + pbase), pl = tr2(pb + 2 * HX_IMG + pbase);
 #pragma unroll
         for (int t9 = 0; t9 < 9; ++t9) {
             const int row0 = (t9 / 3) * 18 + (t9 % 3);
-            const wg_bf16x8 qh = frag(pb, row0, ci * 32), qm = frag(pb + HX_IMG, row0, ci * 32),
-                            ql = frag(pb + 2 * HX_IMG, row0, ci * 32);
+            const char* xa = pb + xb[row0 & 3] + (row0 & ~3) * 128;
+            const wg_bf16x8 qh = tr2(xa), qm = tr2(xa + HX_IMG), ql = tr2(xa + 2 * HX_IMG);
             f32x16 c = acc[t9];
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm, c, 0, 0, 0);   // small terms first
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph, c, 0, 0, 0);
@@ -948,13 +952,31 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph, c, 0, 0, 0);
             acc[t9] = c;
         }
+    };
+    auto step = [&](int t, auto bufc) {       // MFMAs of stage t (buffer t & 1), split stage t+1
+        constexpr int buf = decltype(bufc)::value;
+        mfma_stage(bufc);
         if (t + 1 < T) {
-            split_store((t + 1) & 1);         // raw(t+1) has been in flight for a whole stage
+            split_store(buf ^ 1);             // raw(t+1) has been in flight for a whole stage
             load(t + 2);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+    };
+
+    if (T > 0) {
+        load(0);
+        split_store(0);
+        load(1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
+    int t = 0;
+    for (; t + 1 < T; t += 2) {
+        step(t, std::integral_constant<int, 0>{});
+        step(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < T) step(t, std::integral_constant<int, 0>{});
 
     float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
     if (bias_blk) {                           // column sums of dZ: 16 rows of partials per column

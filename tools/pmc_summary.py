@@ -7,7 +7,7 @@ for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), rec
         name = r.get("Kernel_Name", r.get("KernelName", "?"))
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for name, cs in acc.items():
-    if "igemm" not in name and "wgrad_kernel" not in name:
+    if "igemm" not in name and "wgrad" not in name:
         continue
     print(name)
     for c, v in sorted(cs.items()):
