@@ -261,6 +261,9 @@ int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit
 size_t pu_wgrad_bf16_workspace_bytes(const pu_wgrad_args* a);
 int pu_wgrad_bf16(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);
 int pu_wgrad_bf16_phase(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, int phase, void* stream);
+/* the weight-gradient plan for these arguments: tile (bn x bk), *halo = 1 when the 3x3/s1 halo-reuse
+ * kernel runs (64-channel multiples, out_w % 16 == 0), pixel-row splits */
+int pu_wgrad_bf16_tile(const pu_wgrad_args* a, int* bn, int* bk, int* halo, int* splits);
 int pu_pack_weight_bf16(const float* w, void* packed, int mode, int d0, int d1, int kh, int kw,
                         int k_pad, int cgroup, void* stream);
 int pu_convert_f32_bf16(const float* x, void* y, long long n, void* stream);

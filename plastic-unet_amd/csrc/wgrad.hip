@@ -1230,6 +1230,9 @@ static bool small_wgrad_ok(const pu_wgrad_args* a) {
 #ifndef PU_WG_FQ
 #define PU_WG_FQ 1         // stride-1 same-size layers: scalar + compare-and-wrap Q addressing
 #endif
+#ifndef PU_WG_HALO_BF16
+#define PU_WG_HALO_BF16 1  // the same layers in bf16 (config C3): wgrad_halo_bf16_kernel
+#endif
 #ifndef PU_WG_HALO
 #define PU_WG_HALO 1       // 3x3/s1 layers with 64-channel multiples: halo-reuse kernel (wgrad_halo_x6_kernel)
 #endif
@@ -1578,6 +1581,184 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const WgradBf16Params p
     }
 }
 
+// ------------------------------------------ bf16 weight gradient with halo reuse (3x3/s1, C3)
+// The bf16 form of wgrad_halo_x6_kernel: the operands already are bf16, so a stage's 3 x 18 halo
+// (54 pixel rows x 64 channels = 128 B per row) and its 16 dZ rows go to ONE LDS plane as they
+// arrive, and each tap is one v_mfma_f32_32x32x16_bf16 per wave instead of an im2col image per
+// tap (wgrad_bf16_kernel stages 9 shifted copies of every pixel).  Same swizzle (hx_off), same
+// transposed reads, same 4-wave (channel half, output half) x 9-tap accumulator layout, same
+// slab partials.  Two stages (32 output pixels) per barrier: the bf16 MFMA work of one stage
+// (9 x 32 cycles per wave) is too short to hide a barrier.  Requirements as the x6 kernel.
+constexpr int HB_IMG = (HX_ROWS + 16) * 128;  // bytes of one stage's plane (X rows, then 16 dZ rows)
+
+__global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Params p) {
+    constexpr int XG = 4;                     // halo row groups per thread (54 rows = 3 x 16 + 6)
+    constexpr int SPB = 2;                    // stages per barrier
+    __shared__ __attribute__((aligned(16))) char lds[2 * SPB * HB_IMG];
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ci = wave & 1, nj = wave >> 1;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % p.gx;               // 64-channel input tile
+    const int tyz = tile / p.gx;
+    const int ty = tyz % p.gy;                // 64-channel output tile
+    const int tz = tyz / p.gy;
+    const int m_begin = tz * p.mps;
+    const int m_end = min(p.M, m_begin + p.mps);
+    const int T = m_end > m_begin ? (m_end - m_begin) / 16 : 0;
+
+    const int cq = tid & 15;                  // 4-channel quad of the row this thread loads
+    const int c_lo = tx * 64;
+    const bool first = c_lo < p.c0;
+    const __bf16* xsrc = first ? p.src0 + c_lo : p.src1 + (c_lo - p.c0);
+    const int cs = first ? p.c0 : p.c1;
+    const __bf16* zero = reinterpret_cast<const __bf16*>(g_wg_zero16);
+    const __bf16* x_lane[XG];
+    unsigned x_cls[XG];                       // edge classes: 1 top, 2 bottom, 4 left, 8 right, 16 past the halo, 32 all
+#pragma unroll
+    for (int i = 0; i < XG; ++i) {
+        const int hp = (tid >> 4) + 16 * i;
+        const int rr = hp / 18, cc = hp - rr * 18;
+        x_lane[i] = xsrc + (long long)((rr - 1) * p.Wi + (cc - 1)) * cs + cq * 4;
+        if (hp >= HX_ROWS) x_lane[i] = zero;
+        x_cls[i] = 32u | (hp >= HX_ROWS ? 16u
+                                        : ((rr == 0 ? 1u : 0u) | (rr == 2 ? 2u : 0u) | (cc == 0 ? 4u : 0u) | (cc == 17 ? 8u : 0u)));
+    }
+    const __bf16* p_lane = p.P + (long long)(tid >> 4) * p.N + ty * 64 + cq * 4;
+
+    u32x2 rx[SPB][XG], rp[SPB];
+    auto load = [&](int t, int j) {           // raw bf16 rows of stage t into register set j
+        const int m0 = m_begin + 16 * t;
+        const int tu = fdiv(m0, p.dWo);
+        const int wo0 = m0 - tu * p.Wo;
+        const int bu = fdiv(tu, p.dHo);
+        const int ho = tu - bu * p.Ho;
+        const bool live = t < T;
+        const unsigned flags = live ? (16u | (ho == 0 ? 1u : 0u) | (ho == p.Ho - 1 ? 2u : 0u) | (wo0 == 0 ? 4u : 0u) |
+                                       (wo0 + 16 == p.Wo ? 8u : 0u))
+                                    : 0xffffffffu;
+        const unsigned xo = __umul24((unsigned)m0, (unsigned)cs);
+#pragma unroll
+        for (int i = 0; i < XG; ++i) {
+            const __bf16* g = (x_cls[i] & flags) ? zero : x_lane[i] + xo;
+            rx[j][i] = *reinterpret_cast<const u32x2*>(g);
+        }
+        const __bf16* gp = live ? p_lane + __umul24((unsigned)m0, (unsigned)p.N) : zero;
+        rp[j] = *reinterpret_cast<const u32x2*>(gp);
+    };
+    f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
+    const bool bias_blk = p.bias_mode == 1 && tx == 0;
+    const int w_base = hx_off(tid >> 4, cq * 4);
+    const int wp_base = hx_off(HX_ROWS + (tid >> 4), cq * 4);
+    auto store = [&](int buf, int j, bool live) {   // register set j -> plane j of buffer buf
+        char* pb = lds + (buf * SPB + j) * HB_IMG;
+#pragma unroll
+        for (int i = 0; i < XG; ++i) {
+            const int hp = (tid >> 4) + 16 * i;
+            if (i < 3 || hp < HX_ROWS) *reinterpret_cast<u32x2*>(pb + w_base + i * 16 * 128) = rx[j][i];
+        }
+        *reinterpret_cast<u32x2*>(pb + wp_base) = rp[j];
+        if (bias_blk && live) {
+            bsum[0] += __builtin_bit_cast(float, rp[j][0] << 16);
+            bsum[1] += __builtin_bit_cast(float, rp[j][0] & 0xffff0000u);
+            bsum[2] += __builtin_bit_cast(float, rp[j][1] << 16);
+            bsum[3] += __builtin_bit_cast(float, rp[j][1] & 0xffff0000u);
+        }
+    };
+
+    f32x16 acc[9];
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t9][r] = 0.f;
+
+    const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
+    const int rsub = 8 * (grp >> 1) + gq;
+    const int ccol = 16 * (grp & 1) + 4 * gp;
+    int xb[4];
+#pragma unroll
+    for (int res = 0; res < 4; ++res) xb[res] = hx_off(res + rsub, ci * 32 + ccol);
+    const int pbase = hx_off(HX_ROWS + rsub, nj * 32 + ccol);
+    auto tr2 = [&](const char* a) {
+        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a);
+        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a + 4 * 128));
+        typedef short wi16x8 __attribute__((ext_vector_type(8)));
+        const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        return __builtin_bit_cast(wg_bf16x8, av);
+    };
+    auto mfma_plane = [&](const char* pb) {
+        const wg_bf16x8 ph = tr2(pb + pbase);
+#pragma unroll
+        for (int t9 = 0; t9 < 9; ++t9) {
+            const int row0 = (t9 / 3) * 18 + (t9 % 3);
+            const wg_bf16x8 qh = tr2(pb + xb[row0 & 3] + (row0 & ~3) * 128);
+            acc[t9] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph, acc[t9], 0, 0, 0);
+        }
+    };
+    // group g = stages SPB g .. SPB g + SPB - 1 in buffer g & 1; the loads of group g + 1 are in
+    // flight while group g's MFMAs run
+    const int NG = (T + SPB - 1) / SPB;
+    auto group = [&](int g, auto bufc) {
+        constexpr int buf = decltype(bufc)::value;
+#pragma unroll
+        for (int j = 0; j < SPB; ++j) mfma_plane(lds + (buf * SPB + j) * HB_IMG);
+        if (g + 1 < NG) {
+#pragma unroll
+            for (int j = 0; j < SPB; ++j) store(buf ^ 1, j, SPB * (g + 1) + j < T);
+#pragma unroll
+            for (int j = 0; j < SPB; ++j) load(SPB * (g + 2) + j, j);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+
+    if (NG > 0) {
+#pragma unroll
+        for (int j = 0; j < SPB; ++j) load(j, j);
+#pragma unroll
+        for (int j = 0; j < SPB; ++j) store(0, j, j < T);
+#pragma unroll
+        for (int j = 0; j < SPB; ++j) load(SPB + j, j);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    int g = 0;
+    for (; g + 1 < NG; g += 2) {
+        group(g, std::integral_constant<int, 0>{});
+        group(g + 1, std::integral_constant<int, 1>{});
+    }
+    if (g < NG) group(g, std::integral_constant<int, 0>{});
+
+    float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
+    if (bias_blk) {
+        f32x4* red = reinterpret_cast<f32x4*>(lds);
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < 16) {
+            f32x4 v = red[tid];
+            for (int r = 1; r < 16; ++r) v += red[r * 16 + tid];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) slab[(long long)(ty * 64 + tid * 4 + e) * p.Kcp + p.K] = v[e];
+        }
+    }
+    const int lr = lane & 31, lh = lane >> 5;
+    const int n = ty * 64 + nj * 32 + lr;
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = t9 * p.C + c_lo + ci * 32 + 8 * q + 4 * lh;
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[t9][4 * q + e];
+            *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
+        }
+    }
+}
+
 // phase 2 of every weight-gradient path: fixed-order fp64 reduction of the split partials and
 // the scatter into PyTorch's [n][c][kh][kw] (+ bias)
 static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* workspace, hipStream_t s) {
@@ -1626,7 +1807,23 @@ static int plan_wgrad_bf16(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->Nr = a->n + (a->bias_mode == 2 ? 1 : 0);
     pl->Kc = pl->K + (a->bias_mode == 1 ? 1 : 0);
     pl->Kcp = (pl->Kc + 3) / 4 * 4;
-    pl->qvec = true; pl->dma = true; pl->small = false;
+    pl->qvec = true; pl->dma = true; pl->small = false; pl->x6p = false;
+    pl->halo = PU_WG_HALO_BF16 && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->out_h &&
+               a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 && a->n % 64 == 0 &&
+               a->bias_mode != 2 && M * pl->C < (1LL << 31);
+    if (pl->halo) {                   // wgrad_halo_bf16_kernel: 64 x 64 x 9-tap tiles, two blocks per CU
+        pl->BN = 64; pl->BK = 9 * 64;
+        pl->gx = pl->C / 64;
+        pl->gy = a->n / 64;
+        const int stages = (int)(M / 16);
+        int splits = 512 / (pl->gx * pl->gy);
+        if (splits > stages) splits = stages;
+        if (splits < 1) splits = 1;
+        pl->mps = ceil_div(stages, splits) * 16;
+        pl->splits = ceil_div((int)M, pl->mps);
+        plan_groups(pl);
+        return PU_OK;
+    }
     pl->BN = WB_W; pl->BK = WB_W;
     pl->gx = ceil_div(pl->K, WB_W);
     pl->gy = ceil_div(a->n, WB_W);
@@ -1772,12 +1969,24 @@ extern "C" int pu_wgrad_bf16_phase(const pu_wgrad_args* a, void* workspace, size
         p.slab = (float*)workspace; p.mps = pl.mps; p.gx = pl.gx; p.gy = pl.gy;
         p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
         p.dC = make_fastdiv(pl.C); p.dKw = make_fastdiv(a->kw);
-        hipLaunchKernelGGL(wgrad_bf16_kernel, dim3(pl.gx * pl.gy * pl.splits), dim3(256), 0, s, p);
+        if (pl.halo) hipLaunchKernelGGL(wgrad_halo_bf16_kernel, dim3(pl.gx * pl.gy * pl.splits), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(wgrad_bf16_kernel, dim3(pl.gx * pl.gy * pl.splits), dim3(256), 0, s, p);
         st = check_launch("pu_wgrad_bf16 (gemm)");
         if (st != PU_OK) return st;
     }
     if (!(phase & 2)) return PU_OK;
     return wgrad_reduce(pl, a, workspace, s);
+}
+
+extern "C" int pu_wgrad_bf16_tile(const pu_wgrad_args* a, int* bn, int* bk, int* halo, int* splits) {
+    WgradPlan pl;
+    int st = plan_wgrad_bf16(a, &pl);
+    if (st != PU_OK) return st;
+    if (bn) *bn = pl.BN;
+    if (bk) *bk = pl.BK;
+    if (halo) *halo = pl.halo ? 1 : 0;
+    if (splits) *splits = pl.splits;
+    return PU_OK;
 }
 
 extern "C" int pu_wgrad_bf16(const pu_wgrad_args* a, void* workspace, size_t ws_bytes, void* stream) {

@@ -80,6 +80,8 @@ SIGNATURES = [
     ("pu_wgrad_bf16_workspace_bytes", c_size, [ctypes.POINTER(WgradArgs)]),
     ("pu_wgrad_bf16", c_int, [ctypes.POINTER(WgradArgs), P, c_size, P]),
     ("pu_wgrad_bf16_phase", c_int, [ctypes.POINTER(WgradArgs), P, c_size, c_int, P]),
+    ("pu_wgrad_bf16_tile", c_int, [ctypes.POINTER(WgradArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                   ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_pack_weight_bf16", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_convert_f32_bf16", c_int, [P, P, c_ll, P]),
     ("pu_convert_bf16_f32", c_int, [P, P, c_ll, P]),

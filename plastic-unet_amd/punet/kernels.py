@@ -225,7 +225,11 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
             check(L.pu_wgrad_bf16(ctypes.byref(a), ws.data_ptr(), nbytes, _stream()), "pu_wgrad_bf16")
             return
         M = batch * out_hw[0] * out_hw[1]
-        with _Rec("wgrad_bf16<128x128>", flops=2.0 * M * n * k * k * (c0 + c1)):
+        bn, bk, hl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(L.pu_wgrad_bf16_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(hl), None),
+              "pu_wgrad_bf16_tile")
+        tag = "wgrad_bf16<%dx%d%s>" % (bn.value, bk.value, ",halo" if hl.value else "")
+        with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
             check(L.pu_wgrad_bf16_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 1, _stream()), "pu_wgrad_bf16")
         with _Rec("wgrad_reduce", nbytes=float(nbytes)):
             check(L.pu_wgrad_bf16_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 2, _stream()), "pu_wgrad_bf16")

@@ -60,6 +60,10 @@ CASES = [
     (3, 12, 20, 32, 32, 32),      # non-square, N = 32
     (1, 4, 4, 128, 64, 64),       # tiny pixel grid: split-K + bf16 reduce epilogue
     (2, 33, 17, 96, 0, 96),       # ragged tiles, 96 channels
+    # halo-reuse wgrad (64-channel multiples, width % 16 == 0): edges, concat, odd stage counts
+    (3, 7, 32, 64, 64, 64),       # 7 rows: every stage touches the top or bottom edge
+    (1, 5, 48, 128, 0, 192),      # 15 stages, 2 x 3 channel tiles
+    (2, 64, 64, 64, 0, 64),       # 512 stages over 512 splits
 ]
 
 
