@@ -194,7 +194,9 @@ def main():
     device = torch.device("cuda", local)
 
     from punet import kernels as K
+    from punet import _lib
     from punet.engine import Trainer
+    build_id = _lib.build_id()
 
     torch.manual_seed(0)
     net = build_model(args, device)
@@ -283,14 +285,18 @@ def main():
                          "mfma_tflop_s": round(ach, 2),
                          "peak_basis": "HBM3E 8 TB/s (MI355X_MICROARCH.md); direct small-channel conv, "
                                        "algorithmic bytes = inputs + outputs + masks"})
+        # HBM bytes per launch from the PMC passes (tools/pmc_traffic.py), only when they were
+        # taken on this very build (same pu_build_id); otherwise null
         prof_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        roof["traffic_source"] = None
         if os.path.exists(prof_path):
-            try:
-                tr = json.load(open(prof_path)).get(dtag)
-                if tr:
-                    roof["traffic"] = tr.get("hbm_bytes_per_launch")
-            except Exception:
-                pass
+            pmc = json.load(open(prof_path))
+            tr = pmc.get("kernels", {}).get(dtag) if pmc.get("build_id") == build_id else None
+            if tr:
+                roof["traffic"] = tr.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = "profiles/pmc_traffic.json (build %s, 2*FETCH_SIZE + WRITE_SIZE)" % build_id
+                if tr.get("mfma_busy_frac") is not None:
+                    roof["pmc_mfma_busy_frac"] = tr["mfma_busy_frac"]
 
     oja = None
     if rank == 0 and not args.no_oja:
@@ -322,6 +328,7 @@ def main():
                        {"split6": "fp32 operands split exactly into 3 bf16 terms, 6 bf16 MFMA products per fp32 "
                                   "product, fp32 accumulation (error of an fp32 product)",
                         "native": "v_mfma_f32_32x32x2_f32"}[K.fp32_math()]},
+            "build_id": build_id,
             "final_loss": final_loss,
             "roofline": roof,
             "oja_update": oja,

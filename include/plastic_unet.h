@@ -59,6 +59,10 @@ typedef enum {
 
 int pu_abi_version(void);
 const char* pu_last_error(void);
+/* build id: sha256 prefix over the library sources, this header and the compile flags
+ * (plastic-unet_amd/build_native.py); bench lines and profiles/ carry it so a measurement names
+ * the exact build it was taken on */
+const char* pu_build_id(void);
 /* number of compute units and shader clock (kHz) of `device` (for roofline peaks) */
 int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes);
 

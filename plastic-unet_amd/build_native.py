@@ -8,7 +8,10 @@ Objects go to plastic-unet_amd/build/, the library to plastic-unet_amd/lib/libpl
 import argparse
 import concurrent.futures as cf
 import glob
+import hashlib
+import json
 import os
+import re
 import subprocess
 import sys
 
@@ -18,6 +21,7 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "build")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libplastic_unet.so")
+RESOURCES = os.path.join(BUILD, "resource_usage.json")
 INCLUDE = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -25,6 +29,9 @@ ARCH = "gfx950"
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + INCLUDE, "-I" + CSRC,
           "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
           "-Wno-unused-result"]
+# per-kernel register / scratch report of every compile (kept next to the object, parsed into
+# build/resource_usage.json; tests/test_resources.py fails on any scratch use or spill)
+RPASS = "-Rpass-analysis=kernel-resource-usage"
 
 
 def _newer(src_list, target):
@@ -37,13 +44,62 @@ def _newer(src_list, target):
 def _compile(src, force, defines=(), tag=""):
     obj = os.path.join(BUILD, os.path.basename(src) + tag + ".o")
     deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(INCLUDE, "plastic_unet.h")]
-    if not force and not _newer(deps, obj):
+    if not force and not _newer(deps, obj) and os.path.exists(obj + ".resources.txt"):
         return obj, None
-    cmd = [HIPCC] + CFLAGS + ["-D" + d for d in defines] + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + [RPASS] + ["-D" + d for d in defines] + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, "%s\n%s\n%s" % (" ".join(cmd), r.stdout, r.stderr)
+    with open(obj + ".resources.txt", "w") as f:
+        f.write(r.stderr)
     return obj, None
+
+
+_FIELDS = {"VGPRs": "vgpr", "AGPRs": "agpr", "TotalSGPRs": "sgpr", "ScratchSize [bytes/lane]": "scratch",
+           "Occupancy [waves/SIMD]": "occupancy", "SGPRs Spill": "sgpr_spill", "VGPRs Spill": "vgpr_spill",
+           "LDS Size [bytes/block]": "lds"}
+
+
+def parse_resources(text):
+    """{mangled kernel name: {vgpr, agpr, sgpr, scratch, occupancy, sgpr_spill, vgpr_spill, lds}}
+    from hipcc's -Rpass-analysis=kernel-resource-usage remarks."""
+    out, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark:\s+Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([^:]+): (\S+) \[-Rpass-analysis", line)
+        if m and cur is not None and m.group(1).strip() in _FIELDS:
+            v = m.group(2)
+            cur[_FIELDS[m.group(1).strip()]] = int(v) if v.lstrip("-").isdigit() else v
+    return out
+
+
+def source_hash(defines=()):
+    """Build id: sha256 over every library source, the public header and the compile flags."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")))
+    for f in files + [os.path.join(INCLUDE, "plastic_unet.h")]:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(CFLAGS + list(defines)).encode())
+    return h.hexdigest()[:16]
+
+
+def _build_id_object(bid, tag):
+    """build/build_id<tag>.o exporting pu_build_id() -> the source hash (rewritten when it changes)."""
+    src = os.path.join(BUILD, "build_id%s.cpp" % tag)
+    obj = src[:-4] + ".o"
+    text = 'extern "C" const char* pu_build_id(void) { return "%s"; }\n' % bid
+    if not (os.path.exists(src) and open(src).read() == text and os.path.exists(obj)):
+        with open(src, "w") as f:
+            f.write(text)
+        r = subprocess.run(["g++", "-O2", "-fPIC", "-c", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("build id: %s" % r.stderr)
+    return obj
 
 
 def build(force=False, jobs=None, verbose=True, defines=(), lib=None):
@@ -62,13 +118,25 @@ def build(force=False, jobs=None, verbose=True, defines=(), lib=None):
                 errors.append(err)
     if errors:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
+    bid = source_hash(defines)
+    objs.append(_build_id_object(bid, tag))
+    if not defines:
+        usage = {}
+        for o in objs[:-1]:
+            rep = o + ".resources.txt"
+            if os.path.exists(rep):
+                for k, v in parse_resources(open(rep).read()).items():
+                    v["source"] = os.path.basename(o).split(".hip")[0] + ".hip"
+                    usage[k] = v
+        with open(RESOURCES, "w") as f:
+            json.dump({"build_id": bid, "kernels": usage}, f, indent=1, sort_keys=True)
     if force or _newer(objs, target):
         cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", target] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n%s\n%s" % (r.stdout, r.stderr))
     if verbose:
-        print("built", target)
+        print("built", target, "build id", bid)
     return target
 
 

@@ -1403,8 +1403,7 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
 #define PU_X6_N64 0      // N <= 64 layers: 0 = 256x64 (4 waves), 1 = 512x64 (8 waves), 2 = 128x64 (4x1 waves)
 #endif
 #ifndef PU_X6_BIG
-#define PU_X6_BIG 1      // long-K layers (k_pad >= 2048): 1 = 256x128 8-wave tiles, 2 = also 256x256
-                         // for N >= 256 (measured slower); 0 = 128x128 4-wave tiles everywhere
+#define PU_X6_BIG 1      // long-K layers (k_pad >= 2048): 1 = 256x128 8-wave tiles; 0 = 128x128 4-wave tiles
 #endif
 static bool uses_x6(const pu_conv_args* a);
 #ifndef PU_X6_LEAN
@@ -1439,7 +1438,7 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
         // 8 waves, one block per CU (85 KB of LDS), each wave 32 pixels x 128 channels: fewer
         // LDS-DMA pieces and global bytes per MFMA than two 128 x 128 blocks; +2-4% on the
         // long-K layers (16x16 / 32x32 levels), a loss on short-K ones (K = 576: l2_cat dgrad)
-        *bn = (N >= 256 && PU_X6_BIG > 1) ? 256 : 128;
+        *bn = 128;
         *bm = 256;
         target = 256;
     } else {
@@ -1581,7 +1580,6 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
             else if (bm == 256 && bn == 64) PU_XL(256, 64, 4, 1, 4);
             else if (bm == 128 && bn == 128 && PU_X6_W41) PU_XL(128, 128, 4, 1, 4);
             else if (bm == 128 && bn == 64 && !w41_64) PU_XL(128, 64, 2, 2, 4);
-            else if (bm == 64 && bn == 64) PU_XL(64, 64, 2, 2, 4);
             else done = false;
 #undef PU_XL
             if (done) {
@@ -1593,9 +1591,7 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
             }
         }
 #define PU_X6(BM_, BN_, WM_, WN_) hipLaunchKernelGGL((igemm_x6_kernel<BM_, BN_, WM_, WN_, PU_X6_NBUF, PU_X6_KSUB>), grid, dim3(256), 0, s, p)
-        if (bm == 256 && bn == 256)
-            hipLaunchKernelGGL((igemm_x6_kernel<256, 256, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
-        else if (bm == 256 && bn == 128)
+        if (bm == 256 && bn == 128)
             hipLaunchKernelGGL((igemm_x6_kernel<256, 128, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
         else if (bm == 512)
             hipLaunchKernelGGL((igemm_x6_kernel<512, 64, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);

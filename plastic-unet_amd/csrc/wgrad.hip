@@ -809,16 +809,13 @@ __global__ __launch_bounds__(NW * 64) void wgrad_x6p_kernel(const WgradParams p)
 // outside the image are zero); the planes are double buffered, one barrier per stage.
 // Requires stride 1, pad 1, 3x3, Hi == Ho, Wi == Wo, Wo % 16 == 0, c0 % 64 == c1 % 64 == 0,
 // N % 64 == 0, bias_mode != 2, every source under 2^31 elements.
-#ifndef PU_WG_HALO_PIPE
-#define PU_WG_HALO_PIPE 2  // 0: compiler order; 1: LDS fragment reads one tap ahead; 2: 1 + split interleaved
-#endif
 constexpr int HX_ROWS = 54;                   // halo pixel rows (3 x 18)
 constexpr int HX_IMG = (HX_ROWS + 16) * 128;  // bytes of one plane: X rows, then 16 dZ rows
 __device__ __forceinline__ int hx_off(int row, int col) {   // byte offset in a 64-column plane
     return row * 128 + 16 * ((col >> 3) ^ (((row >> 1) & 1) << 2)) + 2 * (col & 7);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void wgrad_halo_x6_kernel(const WgradParams p) {
+__global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p) {
     constexpr int XG = 4;                     // X float4 groups per thread (864 = 3 x 256 + 96)
     __shared__ __attribute__((aligned(16))) char lds[2 * 3 * HX_IMG];
 
@@ -941,26 +938,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         constexpr int buf = decltype(bufc)::value;
         const char* pb = lds + buf * 3 * HX_IMG;
         const wg_bf16x8 ph = tr2(pb + pbase), pm = tr2(pb + HX_IMG + pbase), pl = tr2(pb + 2 * HX_IMG + pbase);
-        auto xaddr = [&](int t9) {
-            const int row0 = (t9 / 3) * 18 + (t9 % 3);
-            return pb + xb[row0 & 3] + (row0 & ~3) * 128;
-        };
-#if PU_WG_HALO_PIPE >= 1
-        // tap t9 + 1's fragments are read before tap t9's MFMAs issue (software pipeline)
-        wg_bf16x8 nh = tr2(xaddr(0)), nm = tr2(xaddr(0) + HX_IMG), nl = tr2(xaddr(0) + 2 * HX_IMG);
-#endif
 #pragma unroll
         for (int t9 = 0; t9 < 9; ++t9) {
-#if PU_WG_HALO_PIPE >= 1
-            const wg_bf16x8 qh = nh, qm = nm, ql = nl;
-            if (t9 + 1 < 9) {
-                const char* xn = xaddr(t9 + 1);
-                nh = tr2(xn); nm = tr2(xn + HX_IMG); nl = tr2(xn + 2 * HX_IMG);
-            }
-#else
-            const char* xa = xaddr(t9);
+            const int row0 = (t9 / 3) * 18 + (t9 % 3);
+            const char* xa = pb + xb[row0 & 3] + (row0 & ~3) * 128;
             const wg_bf16x8 qh = tr2(xa), qm = tr2(xa + HX_IMG), ql = tr2(xa + 2 * HX_IMG);
-#endif
             f32x16 c = acc[t9];
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm, c, 0, 0, 0);   // small terms first
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph, c, 0, 0, 0);
@@ -970,55 +952,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph, c, 0, 0, 0);
             acc[t9] = c;
         }
-#if PU_WG_HALO_PIPE == 1
-        // pin the pipeline: dZ + tap 0 reads, then (tap t+1 reads, tap t MFMAs) x 8, then tap 8
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-        for (int t9 = 0; t9 < 8; ++t9) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-#endif
-    };
-    // PU_WG_HALO_PIPE 2: the split of stage t+1 (VALU + LDS writes into the other buffer) is
-    // interleaved with stage t's MFMAs instead of following them
-    auto pin_interleaved = [&]() {
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-        for (int t9 = 0; t9 < 8; ++t9) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-        }
     };
     auto step = [&](int t, auto bufc) {       // MFMAs of stage t (buffer t & 1), split stage t+1
         constexpr int buf = decltype(bufc)::value;
-#if PU_WG_HALO_PIPE == 2
-        if (t + 1 < T) {
-            split_store(buf ^ 1);             // raw(t+1) has been in flight for a whole stage
-            mfma_stage(bufc);
-            pin_interleaved();
-            load(t + 2);
-        } else {
-            mfma_stage(bufc);
-        }
-#else
         mfma_stage(bufc);
         if (t + 1 < T) {
             split_store(buf ^ 1);             // raw(t+1) has been in flight for a whole stage
             load(t + 2);
         }
-#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
     };

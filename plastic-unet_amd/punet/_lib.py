@@ -59,6 +59,7 @@ class AdamTensor(ctypes.Structure):
 SIGNATURES = [
     ("pu_abi_version", c_int, []),
     ("pu_last_error", ctypes.c_char_p, []),
+    ("pu_build_id", ctypes.c_char_p, []),
     ("pu_device_info", c_int, [c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_ll)]),
     ("pu_conv_igemm", c_int, [ctypes.POINTER(ConvArgs), P]),
     ("pu_conv_igemm_workspace_bytes", c_size, [ctypes.POINTER(ConvArgs)]),
@@ -138,6 +139,11 @@ def load():
         raise LibraryMissing("libplastic_unet.so ABI %d != 1" % lib.pu_abi_version())
     _lib = lib
     return lib
+
+
+def build_id():
+    """Source hash the loaded library was built from (see build_native.source_hash)."""
+    return load().pu_build_id().decode()
 
 
 def check(rc, what=""):

@@ -1,28 +1,17 @@
 #!/bin/bash
-# GPU-box session: tests, smoke, bench, rocprofv3 summary.  Stops at the first crash/timeout
-# (exit codes other than 0/1), never retries a GPU step.
+# One GPU call: the -m gpu parity suite, the default C2 bench line, then the rocprofv3 kernel-trace
+# stats of the same bench (a separate run: profiled runs clock lower).  Each step has its own time
+# limit and the chain stops at the first failure.
+#   bash tools/gpu_check.sh [tag] [--no-tests]
 set -u
-OUT=gpurun_out
-mkdir -p $OUT
-step() {  # name, timeout, command...
-    local name=$1; local tmo=$2; shift 2
-    echo "== $name" >> $OUT/session.log
-    timeout -k 10 $tmo "$@" > $OUT/$name.log 2>&1
-    local rc=$?
-    echo "== $name exit=$rc" >> $OUT/session.log
-    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >> $OUT/session.log; exit $rc; fi
-    return 0
-}
-MODE=${1:-all}
-if [ "$MODE" = "all" ] || [ "$MODE" = "tests" ]; then
-  step tests 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600
-  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+TAG=${1:-r02}
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+export TMPDIR=/tmp
+if [ "${2:-}" != "--no-tests" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+  tail -3 $OUT/pytest.log
 fi
-if [ "$MODE" = "all" ] || [ "$MODE" = "bench" ]; then
-  step bench 900 python bench.py ${BENCH_ARGS:-}
-fi
-if [ "$MODE" = "all" ] || [ "$MODE" = "prof" ]; then
-  export TMPDIR=/tmp
-  step rocprof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
-fi
-tail -3 $OUT/session.log
+timeout -k 10 300 python bench.py > $OUT/bench_c2.log 2>&1 || { tail -30 $OUT/bench_c2.log; exit 1; }
+tail -1 $OUT/bench_c2.log | cut -c 1-400
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python bench.py --no-cpu-baseline --no-oja > $OUT/bench_rocprof.log 2>&1 || { tail -30 $OUT/bench_rocprof.log; exit 1; }
+echo done

@@ -7,6 +7,8 @@
 bytes of 16-B-per-lane streaming reads (glds included) -> doubled; WRITE_SIZE (KB) is exact for
 16-B stores.  hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE) * 1024, mean over the dispatches.
 Effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration.  Keys are bench.py's kernel tags.
+The output names the build id of the library the passes ran (pu_build_id()); bench.py reports
+roofline.traffic only when that id equals the id of the library it is running.
 """
 import collections
 import csv
@@ -88,7 +90,9 @@ def main():
             # MFMA-busy cycles summed over all SIMDs vs wall cycles x 1024 SIMDs
             e["mfma_busy_frac"] = round((sum(mb) / len(mb)) / ((sum(g) / len(g)) / 8.0 * 1024), 4)
         res[tag] = e
-    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plastic-unet_amd"))
+    from punet import _lib
+    json.dump({"build_id": _lib.build_id(), "kernels": res}, open(out, "w"), indent=1, sort_keys=True)
     for k, v in res.items():
         print("%-28s %s" % (k, v))
 
