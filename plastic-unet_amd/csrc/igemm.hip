@@ -14,16 +14,6 @@
 #include "common.h"
 #include <type_traits>
 
-// Experimental ablations for performance analysis (tools/ablate.sh); 0 in the product build.
-//   1: no global loads in the K loop (LDS tiles keep stale data)   2: no LDS staging stores
-//   3: 1 + 2 (LDS reads + MFMA + barrier only)                      4: 3 without the barrier
-#ifndef PU_ABLATE
-#define PU_ABLATE 0
-#endif
-// 1: use only the register-staged kernel (A/B against the direct-to-LDS one)
-#ifndef PU_NO_DMA
-#define PU_NO_DMA 0
-#endif
 
 namespace pu {
 
@@ -352,7 +342,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
 
     for (int t = 0; t < T; ++t) {
         const int buf = t & 1;
-        if (PU_ABLATE != 1 && PU_ABLATE < 3 && t + 1 < T) load_stage(t + 1);
+        if (t + 1 < T) load_stage(t + 1);
         const float* a = As + buf * BM * IG_LDS;
         const float* b = Bs + buf * BN * IG_LDS;
 #pragma unroll
@@ -374,8 +364,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(const IgemmParams p) {
                         // output channels), so each lane ends with 4 consecutive channels of a pixel
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j][s], fa[i][s], acc[i][j], 0, 0, 0);
         }
-        if (PU_ABLATE != 2 && PU_ABLATE < 3 && t + 1 < T) store_stage(buf ^ 1);
-        if (PU_ABLATE != 4) __syncthreads();
+        if (t + 1 < T) store_stage(buf ^ 1);
+        __syncthreads();
     }
 
     epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
@@ -578,74 +568,36 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
 // co-issues with the MFMAs).  Same loader, ring, swizzle, epilogue and split-K as the fp32 kernel.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
-#ifndef PU_X6_SCALAR_SUB
-#define PU_X6_SCALAR_SUB 0   // 1: residual subtractions as scalar v_sub_f32 (no SLP-packed v_pk_add_f32)
-#endif
-
-__device__ __forceinline__ float x6_sub(float a, float b) {
-#if PU_X6_SCALAR_SUB
-    float r;
-    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-#else
-    return a - b;
-#endif
-}
-
 __device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf16x8_t& h, bf16x8_t& m, bf16x8_t& l) {
 #pragma clang fp contract(off)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const float x = e < 4 ? lo4[e] : hi4[e - 4];
         const __bf16 a = (__bf16)x;
-        const float r = x6_sub(x, (float)a);
+        const float r = x - (float)a;
         const __bf16 b = (__bf16)r;
-        const float q = x6_sub(r, (float)b);
+        const float q = r - (float)b;
         h[e] = a;
         m[e] = b;
         l[e] = (__bf16)q;
     }
 }
 
-#ifndef PU_X6_KSUB
-#define PU_X6_KSUB 1     // 16-k sub-stages per LDS ring slot / barrier (exploration knob)
-#endif
-#ifndef PU_X6_SCHED
-#define PU_X6_SCHED 1    // 0: next-stage loads issued before the MFMAs; 1: after the first sub-tile's
-#endif
-#ifndef PU_X6_NBUF
-#define PU_X6_NBUF 3
-#endif
-#ifndef PU_X6_PRIO
-#define PU_X6_PRIO 0     // s_setprio(1) around each sub-tile's MFMA cluster
-#endif
-#ifndef PU_X6_IL
-#define PU_X6_IL 0       // sched_group_barrier: interleave each MFMA with VALU/SALU work
-#endif
-#ifndef PU_X6_W41
-#define PU_X6_W41 1      // 128x128 tile as 4 waves along M (each 32 pixels x 128 channels): one pixel
-                         // split feeds 4 weight fragments (24 MFMAs), 2x2 waves split twice as much
-#endif
-#ifndef PU_X6_PF
-#define PU_X6_PF 0       // 1: register-prefetched pipeline (stage ts+1 fragments read during stage ts MFMAs)
-#endif
-#ifndef PU_X6_ORDER
-#define PU_X6_ORDER 0    // 0: per pixel fragment split + 6 FN MFMAs; 1: all splits first, term-major MFMAs
-#endif
-
-template <int BM, int BN, int WM, int WN, int NBUF, int KSUB, int NW = 4>
+// 3-deep ring of 16-k stages, one barrier per stage; the loads of stage t+2 are issued after the
+// first pixel fragment's MFMAs of stage t (they then overlap the rest of the stage).
+template <int BM, int BN, int WM, int WN, int NW = 4>
 __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) {
+    constexpr int NBUF = 3;
     constexpr int FM = BM / WM / 32;
     constexpr int FN = BN / WN / 32;
-    constexpr int A_LD = BM / (16 * NW);      // pixel rows: glds per wave per sub-stage (16 rows x 64 B)
-    constexpr int W_TOT = 6 * BN / 64;        // weight planes: glds per block per sub-stage (64 x 16 B)
+    constexpr int A_LD = BM / (16 * NW);      // pixel rows: glds per wave per stage (16 rows x 64 B)
+    constexpr int W_TOT = 6 * BN / 64;        // weight planes: glds per block per stage (64 x 16 B)
     constexpr int W_LD = (W_TOT + NW - 1) / NW;   // per wave (surplus ones load the zero page into a sink)
     constexpr bool SINK = (W_TOT % NW) != 0;
-    constexpr int G = (A_LD + W_LD) * KSUB;   // loads per wave per ring slot
-    constexpr int A_FL = BM * 16;             // floats of one sub-stage's pixel image
-    constexpr int W_FL = BN * 6 * 4;          // float-sized slots of one sub-stage's weight planes
-    constexpr int SUB = A_FL + W_FL;
-    constexpr int STAGE = KSUB * SUB;
+    constexpr int G = A_LD + W_LD;            // loads per wave per ring slot
+    constexpr int A_FL = BM * 16;             // floats of one stage's pixel image
+    constexpr int W_FL = BN * 6 * 4;          // float-sized slots of one stage's weight planes
+    constexpr int STAGE = A_FL + W_FL;
     static_assert(WM * WN == NW && A_LD >= 1, "wave grid");
 
     __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE + (SINK ? 256 : 0)];
@@ -688,7 +640,7 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
         }
     }
     // weight-plane loads: block instruction I = wave + 4j covers entries [64 I, 64 I + 64) of the
-    // sub-stage's [q][BN] image (one plane-half q, contiguous rows -> one coalesced 1 KB read)
+    // stage's [q][BN] image (one plane-half q, contiguous rows -> one coalesced 1 KB read)
     const __bf16* w6 = reinterpret_cast<const __bf16*>(p.wt);
     const __bf16* wrow[W_LD];
 #pragma unroll
@@ -699,12 +651,12 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
         const int n = n_blk + row;
         wrow[j] = (I < W_TOT && n < p.N) ? w6 + ((long long)q * p.N + n) * 8 : nullptr;
     }
-    const long long w_stage = 6LL * p.N * 8;   // bf16 elements per 16-k sub-stage
+    const long long w_stage = 6LL * p.N * 8;   // bf16 elements per 16-k stage
 
     const int t0 = kz * p.t_per;
-    const int T = min(p.k_pad / IG_BK - t0, p.t_per);     // 16-k sub-stages of this split
-    const int TS = (T + KSUB - 1) / KSUB;                  // ring slots
-    auto issue_sub = [&](int tl, float* a_slot) {
+    const int T = min(p.k_pad / IG_BK - t0, p.t_per);     // 16-k stages of this split
+    auto issue = [&](int tl, int slot) {
+        float* a_slot = lds + slot * STAGE;
         const bool live = tl < T;
         const int t = t0 + (live ? tl : 0);
         const int k0 = t * IG_BK;
@@ -737,10 +689,6 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
             __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)dst, 16, 0, 0);
         }
     };
-    auto issue = [&](int ts, int slot) {
-#pragma unroll
-        for (int u = 0; u < KSUB; ++u) issue_sub(ts * KSUB + u, lds + slot * STAGE + u * SUB);
-    };
 
     f32x16 acc[FM][FN];
 #pragma unroll
@@ -755,147 +703,43 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
     const int swz = (lr >> 2) & 3;
     const int pos0 = ((2 * lh) ^ swz) * 4, pos1 = ((2 * lh + 1) ^ swz) * 4;
 
-#if PU_X6_PF
-    // Register-prefetched pipeline: the fragments of stage ts+1 are read from LDS right after the
-    // barrier of iteration ts and land while the MFMAs of stage ts (already in registers) run, so
-    // neither the barrier nor the LDS latency sits in front of an MFMA cluster.  Stage ts+3 is
-    // issued into the slot stage ts was read from (every wave waited for those reads before the
-    // barrier).  Requires KSUB == 1, NBUF == 3.
-    static_assert(KSUB == 1 && NBUF == 3, "PF pipeline");
-    struct Frag {
-        f32x4 xa[FM], xb[FM];
-        bf16x8_t fw[3][FN];
-    };
-    auto read_frags = [&](int ts, Frag& f) {
+#pragma unroll
+    for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(s0, s0);
+
+    for (int ts = 0; ts < T; ++ts) {
+        // ring slot ts landed when only the younger slot's loads are pending
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+        __builtin_amdgcn_s_barrier();
         const float* a = lds + (ts % NBUF) * STAGE;
         const float* wp = a + A_FL;
+        f32x4 xa[FM], xb[FM];
+        bf16x8_t fw[3][FN];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-            f.xa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos0);
-            f.xb[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos1);
+            xa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos0);
+            xb[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos1);
         }
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
             for (int j = 0; j < FN; ++j)
-                f.fw[pl][j] = *reinterpret_cast<const bf16x8_t*>(wp + ((pl * 2 + lh) * BN + b_row0 + j * 32) * 4);
-    };
-    auto mfmas = [&](const Frag& f) {
+                fw[pl][j] = *reinterpret_cast<const bf16x8_t*>(wp + ((pl * 2 + lh) * BN + b_row0 + j * 32) * 4);
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
             bf16x8_t xh, xm, xl;
-            split3_bf16(f.xa[i], f.xb[i], xh, xm, xl);
+            split3_bf16(xa[i], xb[i], xh, xm, xl);
 #pragma unroll
             for (int j = 0; j < FN; ++j) {
                 f32x16 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[1][j], xm, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[2][j], xh, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[0][j], xl, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[1][j], xh, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[0][j], xm, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.fw[0][j], xh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xm, c, 0, 0, 0);   // small terms first
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[2][j], xh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xl, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xm, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xh, c, 0, 0, 0);
                 acc[i][j] = c;
             }
-        }
-    };
-    auto step = [&](int ts, const Frag& cur, Frag& nxt) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");   // stage ts+1 landed
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         // my reads of slot ts done
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        read_frags(ts + 1, nxt);
-        issue(ts + 3, ts % NBUF);
-        mfmas(cur);
-    };
-#pragma unroll
-    for (int s0 = 0; s0 < NBUF; ++s0) issue(s0, s0);
-    Frag f0, f1;
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    read_frags(0, f0);
-    int ts = 0;
-    for (; ts + 1 < TS; ts += 2) {
-        step(ts, f0, f1);
-        step(ts + 1, f1, f0);
-    }
-    if (ts < TS) mfmas(f0);
-    if (false)
-#else
-#pragma unroll
-    for (int s0 = 0; s0 < NBUF - 1; ++s0) issue(s0, s0);
-#endif
-
-    for (int ts = 0; ts < TS; ++ts) {
-        // ring slot ts landed when only the NBUF-2 younger slots' loads are pending
-        if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-        else if (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
-        __builtin_amdgcn_s_barrier();
-        const float* slot = lds + (ts % NBUF) * STAGE;
-#pragma unroll
-        for (int u = 0; u < KSUB; ++u) {
-            const float* a = slot + u * SUB;
-            const float* wp = a + A_FL;
-            f32x4 xa[FM], xb[FM];
-            bf16x8_t fw[3][FN];
-#pragma unroll
-            for (int i = 0; i < FM; ++i) {
-                xa[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos0);
-                xb[i] = *reinterpret_cast<const f32x4*>(a + (a_row0 + i * 32) * 16 + pos1);
-            }
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                for (int j = 0; j < FN; ++j)
-                    fw[pl][j] = *reinterpret_cast<const bf16x8_t*>(wp + ((pl * 2 + lh) * BN + b_row0 + j * 32) * 4);
-            if (PU_X6_SCHED == 0 && u == 0) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
-            if (PU_X6_ORDER == 1) {
-                bf16x8_t xs3[3][FM];
-#pragma unroll
-                for (int i = 0; i < FM; ++i) split3_bf16(xa[i], xb[i], xs3[0][i], xs3[1][i], xs3[2][i]);
-                // terms (w plane, x plane), small first; independent accumulators rotate
-                constexpr int TW[6] = {1, 2, 0, 1, 0, 0};
-                constexpr int TX[6] = {1, 0, 2, 0, 1, 0};
-#pragma unroll
-                for (int tt = 0; tt < 6; ++tt) {
-#pragma unroll
-                    for (int i = 0; i < FM; ++i)
-#pragma unroll
-                        for (int j = 0; j < FN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[TW[tt]][j], xs3[TX[tt]][i], acc[i][j], 0, 0, 0);
-                    if (PU_X6_SCHED == 1 && u == 0 && tt == 1) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
-                }
-                continue;
-            }
-#pragma unroll
-            for (int i = 0; i < FM; ++i) {
-                bf16x8_t xh, xm, xl;
-                split3_bf16(xa[i], xb[i], xh, xm, xl);
-                if (PU_X6_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                for (int j = 0; j < FN; ++j) {
-                    f32x16 c = acc[i][j];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xm, c, 0, 0, 0);   // small terms first
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[2][j], xh, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xl, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[1][j], xh, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xm, c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[0][j], xh, c, 0, 0, 0);
-                    acc[i][j] = c;
-                }
-                if (PU_X6_PRIO) __builtin_amdgcn_s_setprio(0);
-                if (PU_X6_SCHED == 1 && u == 0 && i == 0) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
-            }
-            if (PU_X6_IL) {
-                __builtin_amdgcn_sched_group_barrier(0x100, FM * 2 + FN * 3, 0);
-#pragma unroll
-                for (int q = 0; q < FM * FN * 6; ++q) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x004, 2, 0);
-                }
-            }
+            if (i == 0) issue(ts + NBUF - 1, (ts + NBUF - 1) % NBUF);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1341,16 +1185,10 @@ static void launch_mode(int mode, const IgemmParams& p, dim3 grid, hipStream_t s
 static int blocks_for(long long M, int N, int bm, int bn) { return ceil_div(M, bm) * ceil_div(N, bn); }
 
 // tile choice: the largest tile that still gives >= ~2 blocks per CU (256 CUs)
-#ifndef PU_IG_NBUF
-#define PU_IG_NBUF 3    // exploration knob: LDS ring depth of the direct-to-LDS kernel (3 or 4)
-#endif
-#ifndef PU_N64_BM
-#define PU_N64_BM 256   // exploration knob (tools/variants): M tile for N <= 64 layers
-#endif
 static void choose_tile(long long M, int N, int* bm, int* bn) {
     const int target = 480;
     if (N <= 64) {
-        if (PU_N64_BM == 256 && blocks_for(M, N, 256, 64) >= target) { *bm = 256; *bn = 64; }
+        if (blocks_for(M, N, 256, 64) >= target) { *bm = 256; *bn = 64; }
         else if (blocks_for(M, N, 128, 64) >= target) { *bm = 128; *bn = 64; }
         else { *bm = 64; *bn = 64; }
     } else {
@@ -1382,7 +1220,7 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
     const int T = a->k_pad / IG_BK;
     *ksplit = 1;
     *t_per = T;
-    if (PU_NO_DMA || choose_mode(a->c0, a->c1) != LOAD_CHUNK16 || !vec_epilogue(a)) return;
+    if (choose_mode(a->c0, a->c1) != LOAD_CHUNK16 || !vec_epilogue(a)) return;
     const int occ = (bm == 256) ? 2 : (bm == 128 && bn == 128) ? 3 : 4;   // LDS-limited (3-deep ring)
     const int blocks = blocks_for(M, a->n, bm, bn);
     int ks = (256 * occ) / blocks;
@@ -1396,21 +1234,11 @@ static void plan_split(const pu_conv_args* a, long long M, int bm, int bn, int* 
 // fp32 one for the same loads, so its per-stage fixed cost matters less and its per-block
 // setup/epilogue more: small pixel grids (the 8x8 / 16x16 levels) take the large tiles and split
 // K until ~2 blocks per CU, instead of shrinking the tile to 64x64 (6 MFMAs per wave per stage).
-#ifndef PU_X6_TILES
-#define PU_X6_TILES 1
-#endif
-#ifndef PU_X6_N64
-#define PU_X6_N64 0      // N <= 64 layers: 0 = 256x64 (4 waves), 1 = 512x64 (8 waves), 2 = 128x64 (4x1 waves)
-#endif
-#ifndef PU_X6_BIG
-#define PU_X6_BIG 1      // long-K layers (k_pad >= 2048): 1 = 256x128 8-wave tiles; 0 = 128x128 4-wave tiles
-#endif
+// Measured alternatives (round 1, tools/conv_bench.py): 512x64 8-wave and 128x64 4x1 tiles for
+// the 64-channel layers (-4...-9 %), 256x256 8-wave tiles for N >= 256 (-5 %).
 static bool uses_x6(const pu_conv_args* a);
-#ifndef PU_X6_LEAN
-#define PU_X6_LEAN 1     // igemm_x6_lean_kernel where it applies (0: igemm_x6_kernel everywhere)
-#endif
 static bool lean_ok(const pu_conv_args* a) {
-    if (!PU_X6_LEAN || !uses_x6(a)) return false;
+    if (!uses_x6(a)) return false;
     const int C = a->c0 + a->c1;
     if (a->kh != 3 || a->kw != 3 || !(a->cgroup == 16 || a->cgroup == 32)) return false;
     if (a->c1 != 0 && a->c1 != a->c0) return false;
@@ -1421,7 +1249,7 @@ static bool lean_ok(const pu_conv_args* a) {
     return true;
 }
 static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
-    if (!(PU_X6_TILES && uses_x6(a))) {
+    if (!uses_x6(a)) {
         choose_tile(M, a->n, bm, bn);
         plan_split(a, M, *bm, *bn, ksplit, t_per);
         return;
@@ -1432,9 +1260,7 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
     if (N <= 64) {
         *bn = 64;
         *bm = blocks_for(M, N, 256, 64) >= 480 ? 256 : 128;
-        if (PU_X6_N64 == 1 && blocks_for(M, N, 512, 64) >= 480) { *bm = 512; target = 256; }
-        if (PU_X6_N64 == 2) *bm = 128;   // launched as 4 x 1 waves
-    } else if (PU_X6_BIG && a->k_pad >= 2048) {
+    } else if (a->k_pad >= 2048) {
         // 8 waves, one block per CU (85 KB of LDS), each wave 32 pixels x 128 channels: fewer
         // LDS-DMA pieces and global bytes per MFMA than two 128 x 128 blocks; +2-4% on the
         // long-K layers (16x16 / 32x32 levels), a loss on short-K ones (K = 576: l2_cat dgrad)
@@ -1462,21 +1288,18 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
 
 // the small-channel direct convolution handles: 3x3 / s1 / p1 (same size), C in {1,4,8,12,16},
 // N in {4,8,16}, tap-major weight rows, float4 epilogue
-#ifndef PU_NO_SMALLCONV
-#define PU_NO_SMALLCONV 0
-#endif
 static bool small_conv_ok(const pu_conv_args* a) {
     const int C = a->c0 + a->c1;
     const bool cset = C == 1 || C == 4 || C == 8 || C == 12 || C == 16;
     const bool nset = a->n == 4 || a->n == 8 || a->n == 16;
     const bool nc = (a->n == 4) ? (C == 4 || C == 8 || C == 16) : true;
-    return !PU_NO_SMALLCONV && cset && nset && nc && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
+    return cset && nset && nc && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
            a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) && vec_epilogue(a) &&
            (a->cgroup == 0 || a->cgroup >= C) && (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
 }
 
 static bool uses_x6(const pu_conv_args* a) {
-    return a->weight6 && choose_mode(a->c0, a->c1) == LOAD_CHUNK16 && !PU_NO_DMA && !small_conv_ok(a);
+    return a->weight6 && choose_mode(a->c0, a->c1) == LOAD_CHUNK16 && !small_conv_ok(a);
 }
 
 static size_t split_bytes(long long M, int n, int ksplit) {
@@ -1563,9 +1386,8 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         p.t_per = a->k_pad / IG_BK;
     }
     p.part = (float*)a->workspace;
-    const bool w41_64 = PU_X6_N64 == 2 && bm == 128 && bn == 64;
     const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
-    if (a->weight6 && mode == LOAD_CHUNK16 && !PU_NO_DMA) {
+    if (a->weight6 && mode == LOAD_CHUNK16) {
         p.wt = reinterpret_cast<const float*>(a->weight6);
         PU_REQUIRE(((uintptr_t)a->weight6 & 15) == 0, "pu_conv_igemm: weight6 must be 16-byte aligned");
         if (lean_ok(a)) {
@@ -1578,8 +1400,8 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     } while (0)
             if (bm == 256 && bn == 128) PU_XL(256, 128, 8, 1, 8);
             else if (bm == 256 && bn == 64) PU_XL(256, 64, 4, 1, 4);
-            else if (bm == 128 && bn == 128 && PU_X6_W41) PU_XL(128, 128, 4, 1, 4);
-            else if (bm == 128 && bn == 64 && !w41_64) PU_XL(128, 64, 2, 2, 4);
+            else if (bm == 128 && bn == 128) PU_XL(128, 128, 4, 1, 4);
+            else if (bm == 128 && bn == 64) PU_XL(128, 64, 2, 2, 4);
             else done = false;
 #undef PU_XL
             if (done) {
@@ -1590,25 +1412,18 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
                 return check_launch("pu_conv_igemm (x6 lean)");
             }
         }
-#define PU_X6(BM_, BN_, WM_, WN_) hipLaunchKernelGGL((igemm_x6_kernel<BM_, BN_, WM_, WN_, PU_X6_NBUF, PU_X6_KSUB>), grid, dim3(256), 0, s, p)
+#define PU_X6(BM_, BN_, WM_, WN_) hipLaunchKernelGGL((igemm_x6_kernel<BM_, BN_, WM_, WN_>), grid, dim3(256), 0, s, p)
         if (bm == 256 && bn == 128)
-            hipLaunchKernelGGL((igemm_x6_kernel<256, 128, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
-        else if (bm == 512)
-            hipLaunchKernelGGL((igemm_x6_kernel<512, 64, 8, 1, PU_X6_NBUF, PU_X6_KSUB, 8>), grid, dim3(512), 0, s, p);
+            hipLaunchKernelGGL((igemm_x6_kernel<256, 128, 8, 1, 8>), grid, dim3(512), 0, s, p);
         else if (bm == 256) PU_X6(256, 64, 4, 1);
-        else if (w41_64) PU_X6(128, 64, 4, 1);
-        else if (bm == 128 && bn == 128) {
-            if (PU_X6_W41) PU_X6(128, 128, 4, 1);
-            else PU_X6(128, 128, 2, 2);
-        }
-        else if (bm == 128) PU_X6(128, 64, 2, 2);
-        else PU_X6(64, 64, 2, 2);
+        else if (bm == 128 && bn == 128) PU_X6(128, 128, 4, 1);
+        else PU_X6(128, 64, 2, 2);
 #undef PU_X6
-    } else if (mode == LOAD_CHUNK16 && !PU_NO_DMA) {
-        if (bm == 256) hipLaunchKernelGGL((igemm_dma_kernel<256, 64, 4, 1, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
-        else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 128, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
-        else if (bm == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 64, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((igemm_dma_kernel<64, 64, 2, 2, PU_IG_NBUF>), grid, dim3(256), 0, s, p);
+    } else if (mode == LOAD_CHUNK16) {
+        if (bm == 256) hipLaunchKernelGGL((igemm_dma_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
+        else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 128, 2, 2, 3>), grid, dim3(256), 0, s, p);
+        else if (bm == 128) hipLaunchKernelGGL((igemm_dma_kernel<128, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((igemm_dma_kernel<64, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
     } else if (bm == 256) launch_mode<256, 64, 4, 1>(mode, p, grid, s);
     else if (bm == 128 && bn == 128) launch_mode<128, 128, 2, 2>(mode, p, grid, s);
     else if (bm == 128) launch_mode<128, 64, 2, 2>(mode, p, grid, s);

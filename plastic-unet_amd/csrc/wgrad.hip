@@ -533,269 +533,6 @@ typedef __attribute__((address_space(3))) wi16x4 lds_i16x4_t;
 // swizzle of 16-byte chunks in 256-byte rows: conflict-free ds_read_b64_tr_b16
 __device__ __forceinline__ int wb_sw(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
-// ------------------------------------------------ 6-product weight gradient over bf16 planes
-// The fp32 x6 kernel above splits every MFMA operand fragment in the wave that reads it, with
-// the fragment gathered by 8 strided ds_read_b32: ~12 issued instructions per MFMA on the
-// 128 x 256 tile (waves issue-bound, MFMA busy ~0.35).  Here the fp32 P / Q rows still arrive by
-// LDS-DMA, but each element is split ONCE per block: a split pass reads 4 consecutive fp32 of a
-// row (ds_read_b128), writes the hi / mid / lo bf16 quads (ds_write_b64) into row-major plane
-// images, and the MFMA operands come from those with ds_read_b64_tr_b16 (the transposed reads of
-// wgrad_bf16_kernel: 128-column images, 16-byte chunk ch of row r at ch ^ wb_sw(r)).  One barrier
-// per stage: the split pass of stage t+1 and the MFMAs of stage t share a phase (planes double
-// buffered).  Stride-1 same-size layers (FQ addressing), 8 waves.
-template <int BN, int BK, int WN, int WK, int NW>
-__global__ __launch_bounds__(NW * 64) void wgrad_x6p_kernel(const WgradParams p) {
-    constexpr int FN = BN / WN / 32;
-    constexpr int FK = BK / WK / 32;
-    constexpr int P_ROWS = 256 / BN;
-    constexpr int P_TOT = WG_BM / P_ROWS;
-    constexpr int P_LD = (P_TOT + NW - 1) / NW;
-    constexpr int Q_LD = WG_BM * BK / 256 / NW;
-    constexpr int G = P_LD + Q_LD;
-    constexpr int STAGE = WG_BM * (BN + BK);              // fp32 ring slot (floats)
-    constexpr int SINK = (P_TOT % NW) ? 256 : 0;
-    constexpr int NIMG = BN / 128 + BK / 128;            // 128-column plane images per plane
-    constexpr int IMGB = WG_BM * 256;                     // bytes of one image (16 rows x 256 B)
-    constexpr int PLANES = 3 * NIMG * IMGB;               // bytes of one plane buffer (3 planes)
-    constexpr int GROUPS = WG_BM * (BN + BK) / 4;         // float4 groups per stage
-    constexpr int GPT = (GROUPS + NW * 64 - 1) / (NW * 64);
-    static_assert(WN * WK == NW && P_LD >= 1 && Q_LD >= 1 && BN % 128 == 0 && BK % 128 == 0 && FN >= 1 && FK >= 1,
-                  "x6p tile");
-
-    __shared__ __attribute__((aligned(16))) float lds[3 * STAGE + SINK + 2 * PLANES / 4];
-    char* const planes = reinterpret_cast<char*>(lds + 3 * STAGE + SINK);
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wn = wave % WN, wk = wave / WN;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int tx = tile % p.gx;
-    const int tyz = tile / p.gx;
-    const int ty = tyz % p.gy;
-    const int tz = tyz / p.gy;
-    const int n_blk = ty * BN;
-    const int k_blk = tx * BK;
-    const int m_begin = tz * p.mps;
-    const int m_end = min(p.M, m_begin + p.mps);
-
-    // ---- loader geometry (as wgrad_dma_kernel, FQ addressing)
-    const int p_col = (lane % (BN / 4)) * 4;
-    const int p_dr = lane / (BN / 4);
-    const int pn = n_blk + p_col;
-    const bool p_in = pn < p.N;
-    const float* p_lane = p.P + (long long)p_dr * p.N + pn;
-    // per Q piece j: lane row delta, tap offsets, source stride (0: k past K -> zero page) and
-    // the lane's source pointer at m = 0 (host guarantees every source under 2^31 elements, so
-    // the per-stage offset m * cs is one 24-bit multiply)
-    int q_dr[Q_LD], q_r[Q_LD], q_s[Q_LD], q_row0[Q_LD], q_cs[Q_LD];
-    const float* q_fb[Q_LD];
-#pragma unroll
-    for (int j = 0; j < Q_LD; ++j) {
-        const int base = (wave * Q_LD + j) * 256;
-        const int off = base + 4 * lane;
-        q_row0[j] = base / BK;
-        q_dr[j] = off / BK - q_row0[j];
-        const int qk = min(k_blk + off % BK, p.K - 1);
-        const int tap = fdiv(qk, p.dC);
-        const int c = qk - tap * p.C;
-        const int r = fdiv(tap, p.dKw);
-        const int sq = tap - r * p.kw;
-        const bool first = c < p.c0;
-        const int cs = first ? p.c0 : p.c1;
-        const float* q_ptr = first ? p.src0 + c : p.src1 + (c - p.c0);
-        q_fb[j] = q_ptr + (long long)(q_dr[j] + (r - p.pad) * p.Wi + (sq - p.pad)) * cs;
-        q_cs[j] = (k_blk + off % BK < p.K) ? cs : 0;
-        q_r[j] = r - p.pad;
-        q_s[j] = sq - p.pad;
-    }
-
-    auto issue = [&](int m0, int slot) {
-        float* ps = lds + slot * STAGE;
-        float* qs = ps + WG_BM * BN;
-#pragma unroll
-        for (int j = 0; j < P_LD; ++j) {
-            const int I = (P_TOT % NW) ? wave + NW * j : wave * P_LD + j;
-            const int row0 = I * P_ROWS;
-            const int m = m0 + row0 + p_dr;
-            const float* g = g_wg_zero16;
-            float* dst = ps + row0 * BN;
-            if (SINK && I >= P_TOT) dst = lds + 3 * STAGE;
-            else if (m < m_end && p_in) g = p_lane + (long long)(m0 + row0) * p.N;
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)dst, 16, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < Q_LD; ++j) {
-            const int mu = m0 + q_row0[j];
-            const int tu = fdiv(mu, p.dWo);
-            const int wou = mu - tu * p.Wo;
-            const int bu = fdiv(tu, p.dHo);
-            const int hou = tu - bu * p.Ho;
-            int wo = wou + q_dr[j];
-            const bool cw = wo >= p.Wo;
-            wo = cw ? wo - p.Wo : wo;
-            int ho = hou + (cw ? 1 : 0);
-            ho = ho >= p.Ho ? ho - p.Ho : ho;
-            const int hi = ho + q_r[j], wi = wo + q_s[j];
-            const bool ok = mu + q_dr[j] < m_end && q_cs[j] != 0 && (unsigned)hi < (unsigned)p.Hi &&
-                            (unsigned)wi < (unsigned)p.Wi;
-            const float* g = ok ? q_fb[j] + __umul24((unsigned)mu, (unsigned)q_cs[j]) : g_wg_zero16;
-            __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)(qs + (wave * Q_LD + j) * 256), 16, 0, 0);
-        }
-    };
-
-    // ---- split pass: fp32 slot -> plane buffer (row-major 128-column images, swizzled chunks)
-    auto img_off = [](int row, int col) {   // byte offset of (row, col) within one image
-        return row * 256 + 16 * ((col >> 3) ^ wb_sw(row)) + 2 * (col & 7);
-    };
-    auto split_pass = [&](int slot, int buf) {
-        const float* src = lds + slot * STAGE;
-        char* pb = planes + buf * PLANES;
-#pragma unroll
-        for (int i = 0; i < GPT; ++i) {
-            const int g = tid + i * NW * 64;
-            if (GROUPS % (NW * 64) != 0 && g >= GROUPS) break;
-            const bool isp = g < WG_BM * BN / 4;
-            const int gg = isp ? g : g - WG_BM * BN / 4;
-            const int w4 = (isp ? BN : BK) / 4;
-            const int row = gg / w4;
-            const int col = (gg - row * w4) * 4;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(src + (isp ? 0 : WG_BM * BN) + row * (isp ? BN : BK) + col);
-            const int img = isp ? (col >> 7) : BN / 128 + (col >> 7);
-            unsigned h[2], m[2], l[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-#pragma clang fp contract(off)
-                const float x0 = v[2 * q], x1 = v[2 * q + 1];
-                const unsigned a = wg_pk(wg_f32x2{x0, x1});
-                const float r0 = x0 - __builtin_bit_cast(float, a << 16);
-                const float r1 = x1 - __builtin_bit_cast(float, a & 0xffff0000u);
-                const unsigned b = wg_pk(wg_f32x2{r0, r1});
-                const float l0 = r0 - __builtin_bit_cast(float, b << 16);
-                const float l1 = r1 - __builtin_bit_cast(float, b & 0xffff0000u);
-                h[q] = a;
-                m[q] = b;
-                l[q] = wg_pk(wg_f32x2{l0, l1});
-            }
-            char* dst = pb + img * IMGB + img_off(row, col & 127);
-            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<u32x2*>(dst) = u32x2{h[0], h[1]};
-            *reinterpret_cast<u32x2*>(dst + NIMG * IMGB) = u32x2{m[0], m[1]};
-            *reinterpret_cast<u32x2*>(dst + 2 * NIMG * IMGB) = u32x2{l[0], l[1]};
-        }
-    };
-
-    f32x16 acc[FK][FN];
-#pragma unroll
-    for (int i = 0; i < FK; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    // transposed reads (wgrad_bf16_kernel): 16-lane group grp covers columns 16*(grp&1) + 0..15
-    // and rows 8*(grp>>1) + (0..3 | 4..7); lane 4q+p of a group addresses row q, columns 4p..4p+3
-    const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
-    const int row0 = 8 * (grp >> 1) + gq;
-    const int ccol = 16 * (grp & 1) + 4 * gp;
-    auto frag = [&](const char* pb, int pl, int col) {   // col: first plane column of the fragment
-        const char* base = pb + (pl * NIMG + (col >> 7)) * IMGB;
-        const int c = (col & 127) + ccol;
-        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(base + img_off(row0, c)));
-        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(base + img_off(row0 + 4, c)));
-        typedef short wi16x8 __attribute__((ext_vector_type(8)));
-        const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        return __builtin_bit_cast(wg_bf16x8, av);
-    };
-
-    const int T = (m_end > m_begin) ? (m_end - m_begin + WG_BM - 1) / WG_BM : 0;
-    const int bias_w = (p.bias_mode == 1 && tx == 0) ? BN : (p.bias_mode == 2 && ty == 0) ? BK : 0;
-    float bsum = 0.f;
-    auto bias_sum = [&](int slot) {
-        if (tid < bias_w) {
-            const float* img = lds + slot * STAGE + (p.bias_mode == 1 ? 0 : WG_BM * BN);
-#pragma unroll
-            for (int r = 0; r < WG_BM; ++r) bsum += img[r * bias_w + tid];
-        }
-    };
-
-    issue(m_begin, 0);
-    issue(m_begin + WG_BM, 1);
-    issue(m_begin + 2 * WG_BM, 2);
-    if (T > 0) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
-        __builtin_amdgcn_s_barrier();
-        split_pass(0, 0);
-        bias_sum(0);
-    }
-    for (int t = 0; t < T; ++t) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");   // stage t+1 landed
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");         // my plane writes / reads done
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        issue(m_begin + (t + 3) * WG_BM, t % 3);
-        if (t + 1 < T) {
-            split_pass((t + 1) % 3, (t + 1) & 1);
-            bias_sum((t + 1) % 3);
-        }
-        const char* pb = planes + (t & 1) * PLANES;
-        wg_bf16x8 ph[FN], pm[FN], pl[FN];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-            const int col = wn * (BN / WN) + j * 32;
-            ph[j] = frag(pb, 0, col);
-            pm[j] = frag(pb, 1, col);
-            pl[j] = frag(pb, 2, col);
-        }
-#pragma unroll
-        for (int i = 0; i < FK; ++i) {
-            const int col = BN + wk * (BK / WK) + i * 32;
-            const wg_bf16x8 qh = frag(pb, 0, col), qm = frag(pb, 1, col), ql = frag(pb, 2, col);
-#pragma unroll
-            for (int j = 0; j < FN; ++j) {
-                f32x16 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm[j], c, 0, 0, 0);   // small terms first
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pl[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, ph[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pm[j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph[j], c, 0, 0, 0);
-                acc[i][j] = c;
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    float* slab = p.slab + (long long)tz * p.Nr * p.Kcp;
-    if (tid < bias_w) {
-        if (p.bias_mode == 1) {
-            const int n = n_blk + tid;
-            if (n < p.N) slab[(long long)n * p.Kcp + p.K] = bsum;
-        } else {
-            const int k = k_blk + tid;
-            if (k < p.K) slab[(long long)p.N * p.Kcp + k] = bsum;
-        }
-    }
-    const int lr = lane & 31, lh = lane >> 5;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-        const int n = n_blk + wn * (BN / WN) + j * 32 + lr;
-        if (n >= p.N) continue;
-#pragma unroll
-        for (int i = 0; i < FK; ++i) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int k = k_blk + wk * (BK / WK) + i * 32 + 8 * q + 4 * lh;
-                if (k >= p.K) continue;
-                f32x4 v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-                *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
-            }
-        }
-    }
-}
-
 // ------------------------------------------ 6-product weight gradient with halo reuse (3x3/s1)
 // dW[n][tap][c] = sum_m dZ[m][n] * X[m + tap][c].  A stage is 16 consecutive output pixels of one
 // image row; the 9 taps read only the 3 x 18 halo pixels around them, so the block loads and
@@ -1202,49 +939,24 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
 
 struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
-    bool qvec, dma, small, x6p, halo;
+    bool qvec, dma, small, halo;
     int tiles_w, tiles_h;
     size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
     size_t part_bytes() const { return G > 1 ? (size_t)G * Nr * Kcp * sizeof(double) : 0; }
     size_t ws_bytes() const { return ((slab_bytes() + 255) / 256) * 256 + part_bytes(); }
 };
 
-#ifndef PU_NO_SMALLCONV
-#define PU_NO_SMALLCONV 0
-#endif
 static bool small_wgrad_ok(const pu_wgrad_args* a) {
     const int C = a->c0 + a->c1;
-    return !PU_NO_SMALLCONV && (C == 1 || C == 4 || C == 8 || C == 12 || C == 16) &&
+    return (C == 1 || C == 4 || C == 8 || C == 12 || C == 16) &&
            (a->n == 4 || a->n == 8 || a->n == 16) && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
            a->in_h == a->out_h && a->in_w == a->out_w && a->bias_mode != 2 &&
            (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
 }
 
-#ifndef PU_WG_X6_BK256
-#define PU_WG_X6_BK256 1
-#endif
-#ifndef PU_WG_X6_W6
-#define PU_WG_X6_W6 0      // 6-product 64-channel layers with K % 576 == 0 on 64 x 576 tiles, 6 waves: measured
-                           // 6% slower (6 waves on 4 SIMDs; NBUF 2 for two blocks per CU: 15% slower)
-#endif
-#ifndef PU_WG_FQ
-#define PU_WG_FQ 1         // stride-1 same-size layers: scalar + compare-and-wrap Q addressing
-#endif
-#ifndef PU_WG_HALO_BF16
-#define PU_WG_HALO_BF16 1  // the same layers in bf16 (config C3): wgrad_halo_bf16_kernel
-#endif
-#ifndef PU_WG_HALO
-#define PU_WG_HALO 1       // 3x3/s1 layers with 64-channel multiples: halo-reuse kernel (wgrad_halo_x6_kernel)
-#endif
-#ifndef PU_WG_X6P
-#define PU_WG_X6P 0        // N >= 128 stride-1 layers: split-once bf16 planes kernel (wgrad_x6p_kernel)
-#endif
-#ifndef PU_WG_X6_W3
-#define PU_WG_X6_W3 0      // 6-product 64-channel layers with K % 192 == 0 on 64 x 192 tiles as 3 waves of 64 x 64
-#endif
-#ifndef PU_WG_W6_NBUF
-#define PU_WG_W6_NBUF 3    // its LDS ring depth (3: 121 KB, one block per CU; 2: 80 KB, two)
-#endif
+// Measured alternatives (round 1): 64 x 576 6-wave tiles for the 64-channel layers (-6 %), a
+// 3-wave 64 x 192 tile (-8 %), a split-once-planes kernel that still staged fp32 through LDS
+// (-10...-25 %); the halo kernel below replaced all of them on 3x3/s1 layers.
 static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     PU_REQUIRE(a && a->batch > 0 && a->out_h > 0 && a->out_w > 0 && a->in_h > 0 && a->in_w > 0, "pu_wgrad: bad grid");
     PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0, "pu_wgrad: bad taps");
@@ -1263,17 +975,12 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->Kcp = (pl->Kc + 3) / 4 * 4;
     pl->qvec = (a->c0 % 4 == 0) && (a->c1 % 4 == 0);
     pl->small = small_wgrad_ok(a);
-    pl->x6p = false;
     pl->halo = false;
     if (pl->qvec) {
         PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0, "pu_wgrad: sources must be 16-byte aligned");
     }
     PU_REQUIRE(((uintptr_t)a->rows & 15) == 0, "pu_wgrad: rows must be 16-byte aligned");
-#ifdef PU_NO_DMA
-    pl->dma = false;
-#else
     pl->dma = pl->qvec;
-#endif
     if (pl->small) {                   // direct small-channel kernel: one slab row block per block
         pl->tiles_w = ceil_div(a->out_w, SW_TW);
         pl->tiles_h = ceil_div(a->out_h, SW_TH);
@@ -1302,19 +1009,14 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     }
     else { pl->BN = 128; pl->BK = 128; occ = pl->dma ? 3 : 4; }
     // 6-product path: a 128 x 256 tile (2x2 waves of 64 x 128) splits 6 operand fragments per 48
-    // MFMAs instead of 4 per 24, when K pads no worse than with 128 (PU_WG_X6_BK256 knob)
-    if (PU_WG_X6_BK256 && a->math == 1 && pl->dma && pl->BN == 128 &&
+    // MFMAs instead of 4 per 24, when K pads no worse than with 128
+    if (a->math == 1 && pl->dma && pl->BN == 128 &&
         ceil_div(ext_k, 256) * 256 <= ceil_div(ext_k, 128) * 128) {
         pl->BK = 256;
         occ = 2;
     }
-    if (PU_WG_X6_W6 && a->math == 1 && pl->dma && pl->BN == 64 && a->bias_mode != 2 && ext_k % 576 == 0) {
-        pl->BK = 576;
-        occ = PU_WG_W6_NBUF == 3 ? 1 : 2;
-    }
-    pl->x6p = false;
     pl->halo = false;
-    if (PU_WG_HALO && a->math == 1 && pl->dma && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
+    if (a->math == 1 && pl->dma && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
         a->in_h == a->out_h && a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 &&
         a->n % 64 == 0 && a->bias_mode != 2 && (long long)a->batch * a->in_h * a->in_w * (pl->C) < (1LL << 31)) {
         pl->halo = true;
@@ -1337,17 +1039,7 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
         pl->G = G < 1 ? 1 : G;
         return PU_OK;
     }
-    if (PU_WG_X6P && a->math == 1 && pl->dma && pl->BN == 128 && a->stride == 1 && a->in_h == a->out_h &&
-        a->in_w == a->out_w && a->out_w >= 4) {
-        pl->BK = 256;      // wgrad_x6p_kernel<128, 256, 2, 4, 8>: one 8-wave block per CU (144 KB of LDS)
-        pl->x6p = true;
-        occ = 1;
-    }
-    if (PU_WG_X6_W3 && a->math == 1 && pl->dma && pl->BN == 64 && ext_k % 192 == 0) {
-        pl->BK = -192;   // marker: the 3-wave kernel (tile width 192)
-        occ = 4;
-    }
-    pl->gx = ceil_div(ext_k, pl->BK < 0 ? -pl->BK : pl->BK);
+    pl->gx = ceil_div(ext_k, pl->BK);
     pl->gy = ceil_div(ext_n, pl->BN);
     const int tiles = pl->gx * pl->gy;
     // one full round of resident blocks: a grid a few blocks past a multiple of the resident
@@ -1807,8 +1499,8 @@ static int plan_wgrad_bf16(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->Nr = a->n + (a->bias_mode == 2 ? 1 : 0);
     pl->Kc = pl->K + (a->bias_mode == 1 ? 1 : 0);
     pl->Kcp = (pl->Kc + 3) / 4 * 4;
-    pl->qvec = true; pl->dma = true; pl->small = false; pl->x6p = false;
-    pl->halo = PU_WG_HALO_BF16 && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->out_h &&
+    pl->qvec = true; pl->dma = true; pl->small = false;
+    pl->halo = a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->out_h &&
                a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 && a->n % 64 == 0 &&
                a->bias_mode != 2 && M * pl->C < (1LL << 31);
     if (pl->halo) {                   // wgrad_halo_bf16_kernel: 64 x 64 x 9-tap tiles, two blocks per CU
@@ -1853,7 +1545,7 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
     int st = plan_wgrad(a, &pl);
     if (st != PU_OK) return st;
     if (bn) *bn = pl.BN;
-    if (bk) *bk = pl.BK < 0 ? -pl.BK : pl.BK;
+    if (bk) *bk = pl.BK;
     if (qvec) *qvec = pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo kernel
     if (splits) *splits = pl.splits;
     return PU_OK;
@@ -1898,7 +1590,7 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
         phase &= ~1;
     }
     dim3 grid(p.gx * p.gy * pl.splits);
-    const bool fq = PU_WG_FQ && a->stride == 1 && a->in_h == a->out_h && a->in_w == a->out_w && a->out_w >= 4;
+    const bool fq = a->stride == 1 && a->in_h == a->out_h && a->in_w == a->out_w && a->out_w >= 4;
     if (phase & 1) {
 #define PU_WG_DMA(BN_, BK_, WN_, WK_)                                                                    \
     do {                                                                                                     \
@@ -1909,22 +1601,12 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
 #define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
         if (pl.halo) {
             hipLaunchKernelGGL(wgrad_halo_x6_kernel, grid, dim3(256), 0, s, p);
-        } else if (pl.x6p) {
-            hipLaunchKernelGGL((wgrad_x6p_kernel<128, 256, 2, 4, 8>), grid, dim3(512), 0, s, p);
         } else if (pl.dma) {
             if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
             else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
             else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
             else if (pl.BK == 256 && fq) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true, 4, true>), grid, dim3(256), 0, s, p);
             else if (pl.BK == 256) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true>), grid, dim3(256), 0, s, p);
-            else if (pl.BK == -192) {   // 64 x 192 as 3 waves of 64 x 64 (x6, PU_WG_X6_W3)
-                if (fq) hipLaunchKernelGGL((wgrad_dma_kernel<64, 192, 1, 3, 3, true, 3, true>), grid, dim3(192), 0, s, p);
-                else hipLaunchKernelGGL((wgrad_dma_kernel<64, 192, 1, 3, 3, true, 3>), grid, dim3(192), 0, s, p);
-            }
-            else if (pl.BK == 576) {   // bias mode 1 only (its 64 P columns fit the 384 threads)
-                PU_REQUIRE(a->bias_mode != 2, "pu_wgrad: 64 x 576 tile with a column bias");
-                hipLaunchKernelGGL((wgrad_dma_kernel<64, 576, 1, 6, PU_WG_W6_NBUF, true, 6>), grid, dim3(384), 0, s, p);
-            }
             else PU_WG_DMA(128, 128, 2, 2);
         } else if (pl.qvec) {
             if (pl.BK == 64) PU_WG_REG(64, 64, 2, 2, true);
