@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--layers", default=",".join(LAYERS))
     ap.add_argument("--json", default=None)
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad", help="subset of fwd,dgrad,wgrad to time")
     a = ap.parse_args()
     dev = torch.device("cuda")
     cu, clk, _ = K.device_info(0)
@@ -68,11 +69,14 @@ def main():
         pk = T._Packs()
         flops = 2.0 * B * H * H * cout * 9 * (c0 + c1)
         r = {}
-        r["fwd_ms"] = timeit(lambda: T.conv3x3(x0, w, b, pk, x1=x1), a.reps)
-        if c0 > 1:
+        ops = a.ops.split(",")
+        if "fwd" in ops:
+            r["fwd_ms"] = timeit(lambda: T.conv3x3(x0, w, b, pk, x1=x1), a.reps)
+        if c0 > 1 and "dgrad" in ops:
             r["dgrad_ms"] = timeit(lambda: T.conv3x3_dgrad(dz, w, pk, split=c0 if c1 else None, mask0=x0,
                                                            mask1=x1), a.reps)
-        r["wgrad_ms"] = timeit(lambda: T.conv3x3_wgrad(dz, x0, x1), a.reps)
+        if "wgrad" in ops:
+            r["wgrad_ms"] = timeit(lambda: T.conv3x3_wgrad(dz, x0, x1), a.reps)
         for k in ("fwd", "dgrad", "wgrad"):
             if k + "_ms" in r:
                 r[k + "_TF"] = round(flops / (r[k + "_ms"] * 1e-3) / 1e12, 2)
@@ -80,8 +84,8 @@ def main():
         r["gflop"] = flops / 1e9
         res[name] = r
         print("%-8s H=%-3d %4d+%-4d->%-4d  fwd %7.3f ms %6.1f TF | dgrad %7.3f ms %6.1f TF | wgrad %7.3f ms %6.1f TF"
-              % (name, H, c0, c1, cout, r["fwd_ms"], r["fwd_TF"], r.get("dgrad_ms", 0), r.get("dgrad_TF", 0),
-                 r["wgrad_ms"], r["wgrad_TF"]), flush=True)
+              % (name, H, c0, c1, cout, r.get("fwd_ms", 0), r.get("fwd_TF", 0), r.get("dgrad_ms", 0),
+                 r.get("dgrad_TF", 0), r.get("wgrad_ms", 0), r.get("wgrad_TF", 0)), flush=True)
     print("peak fp32 MFMA %.1f TF/s" % peak)
     if a.json:
         json.dump({"peak_TF": peak, "layers": res}, open(a.json, "w"), indent=1)
