@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from punet import bce_loss
-from utils import fast_iou_metric
+from utils import fast_iou_metric, iou_metric_batch
 
 
 def _device_of(net):
@@ -37,6 +37,31 @@ def eval_net(net, X_val, y_val, device, criterion=None, debug=False, batch=32):
                 total_loss += loss.item()
                 total_acc += fast_iou_metric(y_true_in=tf.cpu().numpy(), y_pred_in=yf.cpu().numpy())
     return total_acc / n, total_loss / n
+
+
+def score_model_best_iou(net, X_valid, y_valid, device, debug=False, batch=32):
+    """Threshold search by the best competition IoU (eval.py:20-64): zero-trace forward of every
+    validation sample, 31 thresholds linspace(0.3, 0.7) mapped through the logit as the reference
+    does, iou_metric_batch per threshold; returns (threshold_best, iou_best).
+
+    The reference compares its Python LIST of predictions with a float (eval.py:52), which raises
+    TypeError on Python 3; here the predictions are one array [N, 1, 1, H, W] - the
+    comparison the reference intends - so the search completes."""
+    net.eval()
+    preds = []
+    with torch.no_grad():
+        for s in range(0, len(X_valid), batch):
+            xb = torch.from_numpy(np.asarray(X_valid[s:s + batch], dtype=np.float32)).to(device)
+            y, _ = net(xb, net.initialZeroHebb(xb.shape[0]))
+            preds.append(y.cpu().numpy().reshape(xb.shape[0], 1, 1, y.shape[-2], y.shape[-1]))
+    preds_valid = np.concatenate(preds, 0)
+    thresholds_ori = np.linspace(0.3, 0.7, 31)
+    thresholds = np.log(thresholds_ori / (1 - thresholds_ori))
+    ious = np.array([iou_metric_batch(y_valid, preds_valid > th) for th in thresholds])
+    if debug:
+        print(ious)
+    k = int(np.argmax(ious))
+    return thresholds[k], ious[k]
 
 
 def get_args():

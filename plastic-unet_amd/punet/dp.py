@@ -105,7 +105,7 @@ def allreduce_mean_(tensors, group=None):
 def allreduce_grads(params, gradbuf=None, group=None, bucket_mb=32):
     """Average the gradients of ``params``.  With a GradBuffer that owns every grad, reduce it in
     buckets of ~bucket_mb (reverse order: decoder/head first); otherwise coalesce, reduce, scatter."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return
     if gradbuf is not None and gradbuf.owns_grads():
         n = gradbuf.numel
@@ -136,9 +136,10 @@ class BucketReducer:
     buffer order), then waits: on RCCL ``wait`` only orders the current stream after the
     collective, so the host does not block."""
 
-    def __init__(self, gradbuf, bucket_mb=16, group=None):
+    def __init__(self, gradbuf, bucket_mb=16, group=None, force=False):
         self.gb = gradbuf
         self.group = group
+        self.force = force       # active in a world of one too (exercises the async path)
         cap = max(1, int(bucket_mb * (1 << 20)) // 4)
         self.buckets = []        # [start, end, {param ids}]
         self.bucket_of = {}
@@ -164,7 +165,7 @@ class BucketReducer:
         self.pending = [set(b[2]) for b in self.buckets]
         self.issued = [False] * len(self.buckets)
         self.works = []
-        self.active = dist.is_initialized() and dist.get_world_size(self.group) > 1
+        self.active = dist.is_initialized() and (dist.get_world_size(self.group) > 1 or self.force)
         self.gb.reducer = self if self.active else None
 
     def _issue(self, k):

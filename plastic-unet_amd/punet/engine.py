@@ -18,7 +18,9 @@ from .optim import FusedAdam
 
 class Trainer:
     def __init__(self, net, lr=3e-4, steplr=1e5, gamma=0.666, betas=(0.9, 0.999), eps=1e-8,
-                 flat_grads=True, bucket_mb=16, overlap=True):
+                 flat_grads=True, bucket_mb=16, overlap=True, force_reduce=False):
+        """force_reduce: run the overlapped all-reduce path even in a world of one rank (tests the
+        RCCL async path on a one-GPU box; an AVG over one rank is the identity)"""
         self.net = net
         self.params = list(net.parameters())
         self.opt = FusedAdam(net.parameters(), lr=lr, betas=betas, eps=eps)
@@ -26,7 +28,7 @@ class Trainer:
         self.bucket_mb = bucket_mb
         self.gradbuf = None
         self.reducer = None
-        self.distributed = dist.is_initialized() and dist.get_world_size() > 1
+        self.distributed = dist.is_initialized() and (dist.get_world_size() > 1 or force_reduce)
         if flat_grads and hasattr(net, "_trunk_plan"):
             # flat buffer in gradient-completion order: head (w, alpha), then the trunk's backward order
             trunk = net._trunk_plan()
@@ -37,7 +39,7 @@ class Trainer:
             self.gradbuf = dp.GradBuffer(trainable, next(net.parameters()).device)
             trunk.gradbuf = self.gradbuf
             if self.distributed and overlap:
-                self.reducer = dp.BucketReducer(self.gradbuf, bucket_mb=bucket_mb)
+                self.reducer = dp.BucketReducer(self.gradbuf, bucket_mb=bucket_mb, force=force_reduce)
         self.overlapped_buckets = 0
 
     def step(self, x, t, hebb):

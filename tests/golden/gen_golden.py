@@ -19,6 +19,8 @@ Fixtures (each < 2 MB):
   bce_edge.npz                   BCELoss clamp edge cases (S9)
   train_capture.npz              reference train() for 2 epochs (losses, eval, final params)
   metrics.npz                    fast_iou_metric and RLE encode on fixed masks
+  iou_batch.npz                  iou_metric_batch over logit-space thresholds (eval.py:20-64's
+                                 threshold search, with its S12 list comparison done on an array)
   unetp_{bn,bilinear,bn_bilinear}.npz  UNetp(batch_norm / bilinear_upsample) at 64x64: init, two
                                  train-mode forwards (running statistics), grads, eval forward
   unetpres_bn.npz                UNetpRes(neurons=4, batch_norm=True, dropout 0) at 64x64, the same
@@ -470,6 +472,24 @@ def gen_metrics():
     rles = [encode(np.round(m)) for m in masks]
     save("metrics.npz", yt=yt, yp=yp, iou=np.float64(iou), masks=masks,
          rles=np.array(rles, dtype=object).astype(str))
+
+
+def gen_iou_batch():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_iou_metric", os.path.join(REF, "utils/iou_metric.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    g = np.random.RandomState(21)
+    N = 6
+    y_valid = (g.rand(N, 1, 24, 24) > 0.55).astype(np.float32)
+    y_valid[0] = 0.0                         # empty truth (and below: empty prediction)
+    y_valid[1] = 1.0
+    preds = g.rand(N, 1, 1, 24, 24).astype(np.float32)
+    preds[0] = 0.1
+    preds[2] = y_valid[2][None] * 0.8 + 0.1  # near-perfect prediction
+    thresholds = np.log(np.linspace(0.3, 0.7, 31) / (1 - np.linspace(0.3, 0.7, 31)))
+    ious = np.array([mod.iou_metric_batch(y_valid, preds > th) for th in thresholds])
+    save("iou_batch.npz", y_valid=y_valid, preds=preds, thresholds=thresholds, ious=ious)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,218 @@
+"""BASELINE.json's GPU configurations at their own sizes:
+
+  C3  UNetp depth 5 / base 64, bf16 trunk, 128x128      (B=2 vs the fp64 oracle; bs 32 properties)
+  C4  CoordConv U-Net depth 5 / base 8 / with_r, 256x256 (B=2 vs the fp64 oracle; bs 32 properties)
+  C5  UNetpRes(neurons=8), 512x512                       (B=1 vs the fp64 oracle; bs 16 properties)
+
+The oracle (oracle/ref_cpu.py, pinned to the reference's golden vectors) runs in fp64 at the
+small batch; the full per-GPU batch is checked through size-independent properties: two identical
+steps are bitwise identical (deterministic kernels, fixed-order reductions), every slot of the big
+batch agrees with the same sample run in a small batch (per-slot traces, no cross-slot mixing),
+and the thresholded masks agree bit for bit away from the threshold.
+
+Bars (fp32 configs C4/C5): logits / Y / H' within 1e-4 relative of fp64 (north star), per-tensor
+gradient relative L2 2e-3 (ReLU flips at fp32-noise pre-activations).  bf16 (C3):
+the measured error of a bf16 trunk against fp64 with margin - Y within 5e-5, H' within 5e-6, loss
+within 1e-6, gradient relative L2 per tensor < 0.3 and overall < 0.02 (every bf16 kernel alone
+sits at its rounding bound, tests/test_bf16_gpu.py)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from punet import bce_loss  # noqa: E402
+from unet import UNetp, UNetpRes, CoordConvUNetp  # noqa: E402
+import oracle  # noqa: E402
+
+DEV = torch.device("cuda")
+
+
+def _inputs(B, S, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(B, 1, S, S, generator=g)
+    t = (torch.rand(B, S, S, generator=g) > 0.5).float()
+    H = 0.05 * torch.randn(B, S, S, generator=g)
+    return x, t, H
+
+
+def _step(net, x, t, H):
+    net.zero_grad(set_to_none=True)
+    y, hn = net(x.to(DEV), H.to(DEV))
+    loss = bce_loss(y, t.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().clone() for k, p in net.named_parameters() if p.grad is not None}
+    return y.detach(), hn.detach(), loss.detach(), grads
+
+
+def _oracle_step(ref, x, t, H):
+    ref = ref.double()
+    yr, hr = ref(x.double(), H.double())
+    lr_ = oracle.bce_loss(yr, t.double())
+    lr_.backward()
+    return yr.detach(), hr.detach(), lr_.item(), {k: p.grad for k, p in ref.named_parameters() if p.grad is not None}
+
+
+def _grad_rel(grads, rgrads):
+    rels, num, den = {}, 0.0, 0.0
+    for k, want in rgrads.items():
+        got = grads[k].double().cpu()
+        d = (got - want).norm().item()
+        rels[k] = d / max(want.norm().item(), 1e-30)
+        num += d * d
+        den += want.norm().item() ** 2
+    return rels, (num / max(den, 1e-300)) ** 0.5
+
+
+def _rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).abs().max() / max(b.abs().max().item(), 1e-30)).item()
+
+
+def _masks_agree(y, yr, band=1e-5):
+    """thresholded masks (0.5) equal wherever the oracle is not within `band` of the threshold"""
+    y = y.double().cpu()
+    far = (yr - 0.5).abs() > band
+    assert torch.equal((y > 0.5)[far], (yr > 0.5)[far])
+
+
+def _properties(make, B, S, small, seed, train_masks=None):
+    """bs-B determinism and slot consistency against `small`-slot runs of the same samples"""
+    x, t, H = _inputs(B, S, seed)
+    torch.manual_seed(seed)
+    net = make()
+    if train_masks is not None:
+        train_masks(net)
+    a = _step(net, x, t, H)
+    b = _step(net, x, t, H)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    for k in a[3]:
+        assert torch.equal(a[3][k], b[3][k]), k
+    assert all(torch.isfinite(v).all() for v in a[3].values())
+    for s0 in (0, B - small):
+        sl = slice(s0, s0 + small)
+        ys, hs, _, _ = _step(net, x[sl], t[sl], H[sl])
+        return_y, return_h = a[0][sl], a[1][sl]
+        assert _rel(ys, return_y) < 1e-5, s0
+        assert _rel(hs, return_h) < 1e-5, s0
+    return a
+
+
+# ------------------------------------------------------------------------------------------- C3
+def test_c3_bf16_base64_vs_fp64_oracle():
+    torch.manual_seed(3)
+    ref = oracle.RefUNetp(1, 1, rule="oja", nbf=128, depth=5, base_ch=64)
+    net = UNetp(1, 1, DEV, rule="oja", nbf=128, depth=5, base_ch=64, precision="bf16")
+    net.load_state_dict(ref.state_dict())
+    x, t, H = _inputs(2, 128, 8)
+    y, hn, loss, grads = _step(net, x, t, H)
+    yr, hr, lr_, rg = _oracle_step(ref, x, t, H)
+    ey, eh = (y.double().cpu() - yr).abs().max().item(), (hn.double().cpu() - hr).abs().max().item()
+    rels, tot = _grad_rel(grads, rg)
+    print("C3 bf16 vs fp64: |dY| %.2e |dH| %.2e |dloss| %.2e grad relL2 total %.3f max %.3f"
+          % (ey, eh, abs(loss.item() - lr_), tot, max(rels.values())))
+    # measured on MI355X: |dY| 6.8e-6, |dH| 4.6e-7, |dloss| 1.2e-8, total gradient relative L2
+    # 0.003, worst single tensor 0.12 (a bias whose gradient is a sum of bf16-rounded dZ)
+    assert ey < 5e-5 and eh < 5e-6
+    assert abs(loss.item() - lr_) < 1e-6
+    assert max(rels.values()) < 0.3, rels
+    assert tot < 0.02
+
+
+def test_c3_bf16_bs32_deterministic_and_slot_consistent():
+    """bf16 trunk at its per-GPU batch: bitwise-repeatable steps; Y / H' of a slot equal (to the
+    bf16 trunk's fp32 accumulation-order noise, 1e-5 of max) in a batch of 32 and of 2"""
+    def make():
+        return UNetp(1, 1, DEV, rule="oja", nbf=128, depth=5, base_ch=64, precision="bf16")
+    x, t, H = _inputs(32, 128, 12)
+    torch.manual_seed(12)
+    net = make()
+    a = _step(net, x, t, H)
+    b = _step(net, x, t, H)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    for k in a[3]:
+        assert torch.equal(a[3][k], b[3][k]), k
+    for s0 in (0, 30):
+        ys, hs, _, _ = _step(net, x[s0:s0 + 2], t[s0:s0 + 2], H[s0:s0 + 2])
+        # bf16 activations: a different split-K plan at B=2 can round a few activations the other
+        # way; that reaches Y only through X (w + alpha H), measured < 1e-4
+        assert _rel(ys, a[0][s0:s0 + 2]) < 1e-3, s0
+        assert _rel(hs, a[1][s0:s0 + 2]) < 1e-3, s0
+
+
+# ------------------------------------------------------------------------------------------- C4
+def test_c4_coordconv_depth5_256_vs_fp64_oracle():
+    torch.manual_seed(21)
+    ref = oracle.RefCoordConvUNetp(1, 1, rule="oja", nbf=256, base_ch=8, with_r=True, depth=5)
+    torch.manual_seed(21)
+    net = CoordConvUNetp(1, 1, DEV, rule="oja", nbf=256, base_ch=8, with_r=True, depth=5)
+    for (k, a), (_, b) in zip(net.state_dict().items(), ref.state_dict().items()):
+        assert torch.equal(a.cpu(), b), k
+    x, t, H = _inputs(2, 256, 4)
+    y, hn, loss, grads = _step(net, x, t, H)
+    yr, hr, lr_, rg = _oracle_step(ref, x, t, H)
+    assert _rel(y, yr) < 1e-4 and _rel(hn, hr) < 1e-4
+    assert abs(loss.item() - lr_) < 1e-4 * abs(lr_)
+    _masks_agree(y, yr)
+    rels, tot = _grad_rel(grads, rg)
+    assert max(rels.values()) < 2e-3, rels
+
+
+def test_c4_coordconv_bs32_properties():
+    _properties(lambda: CoordConvUNetp(1, 1, DEV, rule="oja", nbf=256, base_ch=8, with_r=True, depth=5),
+                32, 256, 2, 6)
+
+
+# ------------------------------------------------------------------------------------------- C5
+def test_c5_unetpres_n8_512_vs_fp64_oracle():
+    """eval mode (Dropout2d inactive): forward, loss and every gradient at 512x512"""
+    torch.manual_seed(31)
+    ref = oracle.RefUNetpRes(1, 1, neurons=8, rule="oja", nbf=512)
+    net = UNetpRes(1, 1, DEV, neurons=8, rule="oja", nbf=512)
+    net.load_state_dict(ref.state_dict())
+    ref.eval()
+    net.eval()
+    x, t, H = _inputs(1, 512, 9)
+    y, hn, loss, grads = _step(net, x, t, H)
+    yr, hr, lr_, rg = _oracle_step(ref, x, t, H)
+    assert _rel(y, yr) < 1e-4 and _rel(hn, hr) < 1e-4
+    assert abs(loss.item() - lr_) < 1e-4 * abs(lr_)
+    _masks_agree(y, yr)
+    rels, tot = _grad_rel(grads, rg)
+    assert max(rels.values()) < 2e-3, rels
+
+
+def test_c5_unetpres_bs16_train_properties():
+    """train mode at the per-GPU batch with fixed injected Dropout2d masks (the same per sample in
+    both batch sizes): repeatable and slot-consistent"""
+    B = 16
+    g = torch.Generator().manual_seed(77)
+    masks = {}
+
+    def inject(net):
+        trunk = net._trunk_plan()
+
+        def mask_fn(name, b, c, p):
+            if name not in masks:
+                masks[name] = ((torch.rand(B, c, generator=g) >= p).float() / (1.0 - p)).to(DEV)
+            m = masks[name]
+            return m[inject.sl] if b != B else m
+        trunk.mask_fn = mask_fn
+        net.train()
+    inject.sl = slice(0, B)
+
+    x, t, H = _inputs(B, 512, 13)
+    torch.manual_seed(13)
+    net = UNetpRes(1, 1, DEV, neurons=8, rule="oja", nbf=512)
+    inject(net)
+    a = _step(net, x, t, H)
+    b = _step(net, x, t, H)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    for k in a[3]:
+        assert torch.equal(a[3][k], b[3][k]), k
+    for s0 in (0, B - 1):
+        inject.sl = slice(s0, s0 + 1)
+        ys, hs, _, _ = _step(net, x[s0:s0 + 1], t[s0:s0 + 1], H[s0:s0 + 1])
+        assert _rel(ys, a[0][s0:s0 + 1]) < 1e-5, s0
+        assert _rel(hs, a[1][s0:s0 + 1]) < 1e-5, s0

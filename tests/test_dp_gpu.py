@@ -94,3 +94,59 @@ def test_overlapped_dp_matches_single_process(tmp_path, gpu_device):
             torch.testing.assert_close(r["grads"][0][n], g, rtol=1e-4, atol=1e-5 * sc)
     # per-rank traces are the slots of the single-process run (never synchronised)
     torch.testing.assert_close(torch.cat([r["hebb"] for r in res]), ref["hebb"], rtol=1e-4, atol=1e-6)
+
+
+def _worker_nccl(rank, world, port, out_dir):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    from punet.engine import Trainer
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    net = _ctor(dev)
+    tr = Trainer(net, lr=1e-3, steplr=1e5, bucket_mb=0.05, force_reduce=True)
+    assert tr.reducer is not None
+    xs, ts = _data()
+    hebb = net.initialZeroHebb(B)
+    out = {"loss": [], "grads": [], "overlapped": []}
+    for s in range(STEPS):
+        loss, hebb = tr.step(xs[s].to(dev), ts[s].to(dev), hebb)
+        out["loss"].append(loss.item())
+        out["grads"].append({n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()
+                             if p.grad is not None})
+        out["overlapped"].append(tr.overlapped_buckets)
+    out["params"] = {n: p.detach().cpu().clone() for n, p in net.named_parameters()}
+    torch.save(out, os.path.join(out_dir, "nccl.pt"))
+    dist.destroy_process_group()
+
+
+def test_rccl_async_bucket_path_world1(tmp_path, gpu_device):
+    """The production RCCL path of BucketReducer (ReduceOp.AVG, async_op all-reduces issued from
+    the autograd thread on RCCL's stream, finish() ordering the compute stream by work.wait()) in
+    a world of one rank: AVG over one rank is the identity, so two steps must reproduce the
+    no-reducer run bit for bit - a missing stream dependency would let Adam read gradients the
+    collective is still writing."""
+    from punet.engine import Trainer
+    torch.manual_seed(0)
+    net = _ctor(gpu_device)
+    tr = Trainer(net, lr=1e-3, steplr=1e5)
+    xs, ts = _data()
+    hebb = net.initialZeroHebb(B)
+    ref_loss, ref_grads = [], []
+    for s in range(STEPS):
+        loss, hebb = tr.step(xs[s].to(gpu_device), ts[s].to(gpu_device), hebb)
+        ref_loss.append(loss.item())
+        ref_grads.append({n: p.grad.detach().cpu().clone() for n, p in net.named_parameters() if p.grad is not None})
+    ref_params = {n: p.detach().cpu().clone() for n, p in net.named_parameters()}
+    mp.spawn(_worker_nccl, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    r = torch.load(os.path.join(tmp_path, "nccl.pt"), weights_only=True)
+    assert all(o >= 2 for o in r["overlapped"]), r["overlapped"]
+    assert r["loss"] == ref_loss
+    for s in range(STEPS):
+        for n, g in ref_grads[s].items():
+            assert torch.equal(r["grads"][s][n], g), (s, n)
+    for n, p in ref_params.items():
+        assert torch.equal(r["params"][n], p), n

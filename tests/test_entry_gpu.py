@@ -70,8 +70,8 @@ def test_eval_and_predict_match_oracle(tmp_path):
     racc, rloss = oracle.ref_eval_net(ref, X, Y)
     assert abs(loss - rloss) < 1e-5 * abs(rloss)
     assert abs(acc - racc) < 2e-3
-    rows = infer.predict(net, ["a", "b", "c", "d"], X, {"device": DEV, "mask_threshold": 0.5,
-                                                        "out_dir": str(tmp_path)})
+    rows = infer.predict(net, (["a", "b", "c", "d"], X), {"device": DEV, "mask_threshold": 0.5,
+                                                          "out_dir": str(tmp_path)})
     with open(os.path.join(str(tmp_path), "submission.csv")) as f:
         got = list(csv.reader(f))
     assert got[0] == ["id", "rle_mask"] and len(got) == 5
@@ -82,3 +82,42 @@ def test_eval_and_predict_match_oracle(tmp_path):
             far = np.abs(y.numpy() - 0.5) > 1e-5          # masks bit-exact away from the threshold
             yg = infer.predict_masks(net, x[None], DEV)[0] > 0.5
             assert np.array_equal(yg[far], m[far])
+
+
+def test_start_inference_writes_the_oracles_submission(tmp_path):
+    """infer.start_inference (src/infer.py:110-179): model file -> weights-only load into the
+    reference's UNetpRes(nbf=img_width) -> best-IoU threshold on the validation set -> test-set
+    masks -> RLE CSV; every step checked against the oracle's forward with the same weights."""
+    import pandas as pd
+    import infer
+    from utils import encode, iou_metric_batch
+    N = 32
+    torch.manual_seed(17)
+    ref = oracle.RefUNetpRes(1, 1, nbf=N)                    # reference default neurons=16
+    # a trained-looking head: larger w so the masks are not all ~0.5
+    with torch.no_grad():
+        ref.w.mul_(40.0)
+    path = os.path.join(str(tmp_path), "model.pth")
+    torch.save(ref.state_dict(), path)
+    g = np.random.RandomState(5)
+    X_valid = g.rand(6, 1, N, N).astype(np.float32)
+    y_valid = (g.rand(6, 1, N, N) > 0.5).astype(np.float32)
+    ids = ["img%d" % i for i in range(4)]
+    test_df = pd.DataFrame(index=ids)
+    test_df["images"] = [g.rand(N, N).astype(np.float32) for _ in ids]
+    rows = infer.start_inference(path, test_df, X_valid, y_valid, str(tmp_path), N, N, 1)
+    with open(os.path.join(str(tmp_path), "submission.csv")) as f:
+        got = list(csv.reader(f))
+    assert got[0] == ["id", "rle_mask"] and [r[0] for r in got[1:]] == ids
+    # the oracle's threshold search and masks
+    ref.eval()
+    with torch.no_grad():
+        pv = np.stack([ref(torch.from_numpy(x[None]), ref.initialZeroHebb())[0].numpy()[None, None]
+                       for x in X_valid])
+        th = np.log(np.linspace(0.3, 0.7, 31) / (1 - np.linspace(0.3, 0.7, 31)))
+        ious = np.array([iou_metric_batch(y_valid, pv > t) for t in th])
+        thr = th[int(np.argmax(ious))]
+        for (fn, rle), img in zip(rows, test_df.images):
+            y = ref(torch.from_numpy(img[None, None]), ref.initialZeroHebb())[0].numpy()
+            assert np.abs(y - thr).min() > 1e-5             # no pixel within fp32 noise of the threshold
+            assert rle == encode(np.round(y > thr)), fn

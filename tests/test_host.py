@@ -76,3 +76,13 @@ def test_tgs_loader_layout_split_and_resize(tmp_path):
     assert abs(r[2, 3] - (0.25 * (0.75 * img[0, 1] + 0.25 * img[0, 2]) + 0.75 * (0.75 * img[1, 1] + 0.25 * img[1, 2]))) < 1e-12
     assert abs(r[0, 0] - 0.75 * 0.75 * img[0, 0]) < 1e-12          # (-0.25, -0.25): 3 of 4 neighbours are cval 0
     assert data_set.cov_to_class(0.0) == 0 and data_set.cov_to_class(0.35) == 4 and data_set.cov_to_class(1.0) == 10
+
+
+def test_iou_metric_batch_matches_reference_fixture():
+    """utils.iou_metric_batch vs the reference's iou_metric_batch over the 31 logit-space
+    thresholds of eval.score_model_best_iou (tests/golden/iou_batch.npz), incl. empty masks."""
+    from utils import iou_metric_batch
+    g = golden("iou_batch.npz")
+    got = np.array([iou_metric_batch(g["y_valid"], g["preds"] > th) for th in g["thresholds"]])
+    assert got.dtype == np.float32
+    np.testing.assert_array_equal(got, g["ious"])
