@@ -9,6 +9,8 @@ save checkpoints (:153-203).  Differences, all opt-in:
   --batch-norm / --bilinear  the reference constructor flags batch_norm / bilinear_upsample
   --model-type     unetpres (reference default) | unetp, with --depth/--base-ch for UNetp
   --synthetic N / --dataset FILE.npz   input data besides --data DIR (the TGS PNG layout, utils/data_set.py)
+  --resident       keep the whole training set in HBM; default: batches stream host -> HBM through
+                   pinned, double-buffered asynchronous copies (punet/loader.py) under the previous step
 Data-parallel training: launch with torch.distributed.run; each rank trains its contiguous shard
 of every global batch and gradients are averaged over RCCL.
 Checkpoints: ``{out}/train[_{epoch}]_net.pth`` (state_dict, reference keys), the training parameters
@@ -33,6 +35,7 @@ if HERE not in sys.path:
 from unet import UNetp, UNetpRes  # noqa: E402
 from punet import dp  # noqa: E402
 from punet.engine import Trainer  # noqa: E402
+from punet.loader import BatchPrefetcher  # noqa: E402
 from eval import eval_net  # noqa: E402
 
 
@@ -60,8 +63,15 @@ def train(net, X_train, X_val, y_train, y_val, params):
     samples_count = len(X_train)
     loss_between_saves, last_save_epoch = 0.0, 0
     trainer = Trainer(net, lr=params["lr"], steplr=params["steplr"], gamma=params["gamma"])
-    X_dev = torch.from_numpy(np.asarray(X_train, dtype=np.float32)).to(device)
-    Y_dev = torch.from_numpy(np.asarray(y_train, dtype=np.float32)).to(device)
+    ranges = list(_batches(samples_count, bs, world, rank))
+    if params.get("prefetch", True):
+        # stream batches host -> HBM (pinned, double-buffered, overlapping the previous step)
+        batches = BatchPrefetcher(X_train, y_train, ranges, device)
+    else:
+        # the whole training set resident in HBM (copied once)
+        X_dev = torch.from_numpy(np.asarray(X_train, dtype=np.float32)).to(device)
+        Y_dev = torch.from_numpy(np.asarray(y_train, dtype=np.float32)).to(device)
+        batches = [(X_dev[lo:hi], Y_dev[lo:hi]) for lo, hi in ranges]
     if params["stop_time"] > 0 and verbose:
         print("Training started at: [%s] and set to stop at: [%s]" % (
             datetime.fromtimestamp(time.time()).strftime("%B %d, %Y %H:%M:%S"),
@@ -73,9 +83,8 @@ def train(net, X_train, X_val, y_train, y_val, params):
         # trace reset per epoch (train.py:88): per-slot traces, or one trace threaded through
         hebb = net.initialZeroHebb() if seq else net.initialZeroHebb(bs)
         losses_dev = []
-        for lo, hi in _batches(samples_count, bs, world, rank):
-            x = X_dev[lo:hi]
-            t = Y_dev[lo:hi].reshape(hi - lo, -1)
+        for (lo, hi), (x, yb) in zip(ranges, batches):
+            t = yb.reshape(hi - lo, -1)
             if seq:
                 loss, hebb = trainer.step(x, t, hebb)
             else:
@@ -131,7 +140,7 @@ def start_train(x_train, x_valid, y_train, y_valid, out_dir, model, img_width, i
                 max_train_time=-1, load=False, gpu=True, epochs=5, lr=3e-5, val_ratio=0.05, val_every=50,
                 save_every=100, gamma=0.666, steplr=1e6, rollout=50000, prule="hebb", debug=False,
                 model_type="unetpres", depth=5, base_ch=8, neurons=16, batch_size=1, hebb_mode="slots",
-                batch_norm=False, bilinear_upsample=False):
+                batch_norm=False, bilinear_upsample=False, prefetch=True):
     world, rank, local = dp.init_from_env()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
@@ -139,7 +148,7 @@ def start_train(x_train, x_valid, y_train, y_valid, out_dir, model, img_width, i
     params = {"out_dir": out_dir, "device": device, "epochs": epochs, "stop_time": stop_time, "lr": lr,
               "val_ratio": val_ratio, "val_every": val_every, "save_every": save_every, "rollout": rollout,
               "gamma": gamma, "steplr": steplr, "prule": prule, "im_width": img_width, "im_height": img_height,
-              "im_chan": img_chan, "debug": debug, "batch_size": batch_size}
+              "im_chan": img_chan, "debug": debug, "batch_size": batch_size, "prefetch": prefetch}
     if model_type == "unetp":
         net = UNetp(n_channels=img_chan, n_classes=1, nbf=img_width, batch_norm=batch_norm,
                     bilinear_upsample=bilinear_upsample, device=device, rule=prule, depth=depth, base_ch=base_ch,
@@ -194,6 +203,8 @@ def parse_args(argv=None):
     parser.add_option('--batch-norm', dest='batch_norm', action='store_true', default=False)
     parser.add_option('--bilinear', dest='bilinear', action='store_true', default=False)
     parser.add_option('--seed', dest='seed', type='int', default=0)
+    parser.add_option('--resident', dest='resident', action='store_true', default=False,
+                      help='copy the whole training set to HBM once instead of streaming batches')
     (options, args) = parser.parse_args(argv)
     return options
 
@@ -228,4 +239,4 @@ if __name__ == '__main__':
                 prule=args.prule, img_width=args.img_size, img_height=args.img_size, img_chan=1,
                 debug=args.debug, model_type=args.model_type, depth=args.depth, base_ch=args.base_ch,
                 neurons=args.neurons, batch_size=args.batch_size, hebb_mode=args.hebb_mode,
-                batch_norm=args.batch_norm, bilinear_upsample=args.bilinear)
+                batch_norm=args.batch_norm, bilinear_upsample=args.bilinear, prefetch=not args.resident)

@@ -121,3 +121,25 @@ def test_start_inference_writes_the_oracles_submission(tmp_path):
             y = ref(torch.from_numpy(img[None, None]), ref.initialZeroHebb())[0].numpy()
             assert np.abs(y - thr).min() > 1e-5             # no pixel within fp32 noise of the threshold
             assert rle == encode(np.round(y > thr)), fn
+
+
+def test_streamed_batches_train_identically_to_resident(tmp_path):
+    """train() with the pinned double-buffered H2D prefetcher (default) and with the training set
+    resident in HBM: bitwise the same losses and final parameters (bs 4, ragged last batch,
+    3 epochs; the copies of batch i+1 overlap step i)."""
+    import train
+    g = np.random.RandomState(9)
+    X = g.rand(18, 1, 32, 32).astype(np.float32)
+    Y = (g.rand(18, 1, 32, 32) > 0.5).astype(np.float32)
+    res = []
+    for prefetch in (True, False):
+        torch.manual_seed(4)
+        net = UNetp(1, 1, DEV, rule="oja", nbf=32, depth=4, base_ch=16)
+        params = {"out_dir": str(tmp_path), "device": DEV, "epochs": 3, "stop_time": -1, "lr": 3e-4,
+                  "val_every": 100, "save_every": 100, "rollout": 50000, "gamma": 0.666, "steplr": 4,
+                  "debug": False, "batch_size": 4, "prefetch": prefetch}
+        losses = train.train(net, X, X[:2], Y, Y[:2], params)[0]
+        res.append((losses, {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}))
+    assert res[0][0] == res[1][0]
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k

@@ -86,3 +86,31 @@ def test_iou_metric_batch_matches_reference_fixture():
     got = np.array([iou_metric_batch(g["y_valid"], g["preds"] > th) for th in g["thresholds"]])
     assert got.dtype == np.float32
     np.testing.assert_array_equal(got, g["ious"])
+
+
+def test_batch_prefetcher_order_shards_and_slot_rotation():
+    """punet.loader.BatchPrefetcher on the CPU device (the ordering logic of the GPU pipeline):
+    every yielded batch equals the host slice, ragged last batch included, for depths 2 and 3,
+    float64 / memmapped inputs converted to float32."""
+    import tempfile
+    import torch
+    from punet.loader import BatchPrefetcher
+    from train import _batches
+    g = np.random.RandomState(3)
+    X = g.rand(23, 1, 8, 8)                                   # float64 host data
+    Y = (g.rand(23, 1, 8, 8) > 0.5).astype(np.float32)
+    with tempfile.TemporaryDirectory() as d:
+        mm = np.lib.format.open_memmap(d + "/x.npy", mode="w+", dtype=np.float64, shape=X.shape)
+        mm[:] = X
+        for depth in (2, 3):
+            for bs, world, rank in [(4, 1, 0), (3, 2, 1), (5, 1, 0)]:
+                ranges = list(_batches(len(X), bs, world, rank))
+                pf = BatchPrefetcher(mm, Y, ranges, "cpu", depth=depth)
+                seen = []
+                for (lo, hi), (x, y) in zip(ranges, pf):
+                    assert x.dtype == torch.float32 and x.shape[0] == hi - lo
+                    assert torch.equal(x, torch.from_numpy(X[lo:hi].astype(np.float32)))
+                    assert torch.equal(y, torch.from_numpy(Y[lo:hi]))
+                    seen.append((lo, hi))
+                assert seen == ranges
+    assert list(BatchPrefetcher(X, Y, [], "cpu")) == []
