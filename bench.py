@@ -155,10 +155,10 @@ def _launch_time_us(fn, reps):
         return e0.elapsed_time(e1) * 1e3 / reps, "eager"
 
 
-def oja_update_bench(K, B, N, device):
+def oja_update_bench(K, B, N, device, feat_channels=64):
     """Algorithmic GB/s of the Oja trace update: 8*B*N^2 + 8*B*N bytes (read H, write H', rows),
     the stand-alone kernel at the bench batch (cache-resident) and over an HBM-sized sweep; plus
-    the fused head forward (GEMM + sigmoid + Oja update in one launch, 16*B*N^2 + 8*N^2 bytes)."""
+    the fused head forward (outconv + GEMM + sigmoid + Oja update in one launch)."""
     res = {}
     eta = torch.full((1,), 0.01, device=device)
     sweep = max(1, (1 << 30) // (4 * N * N))            # 1 GiB of traces (16384 at N=128)
@@ -173,14 +173,21 @@ def oja_update_bench(K, B, N, device):
                       "timing": how}
         del H, X, Y, out
     H = 0.1 * torch.randn(B, N, N, device=device)
-    X = torch.randn(B, N, N, device=device)
     w = 0.01 * torch.randn(N, N, device=device)
     a = 0.01 * torch.rand(N, N, device=device)
-    us, how = _launch_time_us(lambda: K.plastic_fwd(X, H, w, a, eta, 1, True), 50)
-    nbytes = 16.0 * B * N * N + 8.0 * N * N
-    res["fused_head_bs%d" % B] = {"us_per_launch": round(us, 3), "bytes": nbytes,
-                                 "GB_s": round(nbytes / us / 1e3, 1),
-                                 "TFLOP_s": round(2.0 * B * N ** 3 / us / 1e6, 2), "timing": how}
+    # the fused head of the training step: outconv (feat [B,N,N,C]) + Weff GEMM + sigmoid + Oja
+    # update in one launch; algorithmic bytes = feat read + X, Y, H' written + H read + w, alpha
+    C = feat_channels
+    feat = torch.rand(B, N, N, C, device=device)
+    wo = 0.1 * torch.randn(C, device=device)
+    bo = torch.zeros(1, device=device)
+    us, how = _launch_time_us(lambda: K.plastic_head_fwd(feat, wo, bo, H, w, a, eta, 1, True), 50)
+    nbytes = 4.0 * B * N * N * C + 16.0 * B * N * N + 8.0 * N * N
+    res["fused_head_bs%d" % B] = {"kernel": "pu_plastic_head_fwd (outconv %d->1 + head + Oja)" % C,
+                                 "us_per_launch": round(us, 3), "bytes": nbytes,
+                                 "GB_s": round(nbytes / us / 1e3, 1), "hbm_frac": round(nbytes / us / 1e3 / 8000.0, 3),
+                                 "TFLOP_s": round((2.0 * B * N ** 3 + 2.0 * B * N * N * C) / us / 1e6, 2),
+                                 "timing": how}
     return res
 
 
@@ -300,7 +307,7 @@ def main():
 
     oja = None
     if rank == 0 and not args.no_oja:
-        oja = oja_update_bench(K, B, S, device)
+        oja = oja_update_bench(K, B, S, device, feat_channels=net.outc.conv.weight.shape[1])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -17,6 +17,8 @@
  *   pu_outconv_fwd/bwd nn.Conv2d(C,1,1) (outconv)      src/unet/unet_p.py:253-260
  *   pu_plastic_fwd     activin.mm(w+alpha*hebb), sigmoid, Hebb/Oja trace update
  *                                                      src/unet/unet_p.py:69-88
+ *   pu_plastic_head_fwd outconv + activin.mm(w+alpha*hebb) + sigmoid + trace update, ONE launch
+ *                                                      src/unet/unet_p.py:67-88
  *   pu_trace_update    the trace update alone          src/unet/unet_p.py:81-86
  *   pu_plastic_bwd     mm/mul/sigmoid backward         (autograd, train.py:110)
  *   pu_bce_fwd/bwd     nn.BCELoss (mean, log >= -100)  src/train.py:70,101-105
@@ -307,6 +309,31 @@ typedef struct {
 int pu_plastic_fwd(const pu_plastic_args* a, void* stream);
 int pu_trace_update(const float* hebb, const float* x, const float* y, const float* eta,
                     float* hebb_out, int batch, int nbf, int rule, void* stream);
+
+/* The fused head of SURVEY 8(b): the 1x1 outconv (unet_p.py:67, 253-260) computed in the head's
+ * prologue from the trunk's last activation feat [B][N][N][C] (NHWC, fp32 or bf16 = feat_bf16),
+ *   X_b[i][k] = sum_c feat[b][i][k][c] out_w[c] + out_b[0]
+ * then Y_b = sigmoid(X_b Weff_b) on v_mfma_f32_16x16x4_f32 (a k-ordered fp32 fma chain) and, when
+ * hebb_out != NULL, the trace update of unet_p.py:81-86 - one launch, grid (N/16, B).  x receives
+ * the logits X (kept for the backward).  Requires N % 16 == 0, C % 4 == 0, 16-byte aligned feat,
+ * hebb_out not aliasing hebb. */
+typedef struct {
+    int batch, nbf, channels;
+    const void* feat;
+    int feat_bf16;
+    const float* out_w;
+    const float* out_b;
+    const float* hebb;
+    const float* w;
+    const float* alpha;
+    const float* eta;
+    float* x;
+    float* y;
+    float* hebb_out;
+    int rule;
+} pu_plastic_head_args;
+
+int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream);
 
 /* backward given dy = dL/dY:  G = dy*(1-y)*y ; dx_b = G_b Weff_b^T ;
  *   dw = sum_b X_b^T G_b ; dalpha = sum_b (X_b^T G_b) (.) H_b   (no gradient to eta: S3) */

@@ -66,6 +66,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
 
 inline int ceil_div(long long a, long long b) { return int((a + b - 1) / b); }
 
+// 4-term dot product as an explicit fma chain (v0 w0 first): the 1x1 outconv's per-lane sum, shared
+// by outconv_fwd_kernel and the fused head so both produce bit-identical logits
+template <typename V>
+__device__ __forceinline__ float dot4_fma(const V v, const V w) {
+    return fmaf(v[3], w[3], fmaf(v[2], w[2], fmaf(v[1], w[1], v[0] * w[0])));
+}
+
 // XCD-aware block order: the dispatcher deals blocks round-robin over the 8 XCDs (block b runs on
 // XCD b % 8).  Map hardware block b to a logical tile so that each XCD gets one CONTIGUOUS range
 // of logical tiles (neighbouring tiles share input rows/halos -> reuse in that XCD's L2).

@@ -204,7 +204,7 @@ __global__ void outconv_fwd_kernel(const T* __restrict__ x, const float* __restr
         for (int c = lane16 * 4; c < C; c += 64) {
             f32x4 v = ld4(x + m * C + c);
             f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
-            s += v[0] * ww[0] + v[1] * ww[1] + v[2] * ww[2] + v[3] * ww[3];
+            s += dot4_fma(v, ww);
         }
         s += __shfl_xor(s, 8, 16);
         s += __shfl_xor(s, 4, 16);

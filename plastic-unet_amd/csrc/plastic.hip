@@ -152,6 +152,165 @@ __global__ void trace_kernel_v4(const float* __restrict__ H, const float* __rest
     reinterpret_cast<f32x4*>(Hn + off)[idx] = out;
 }
 
+
+// ------------------------------------------------------------------- fused head (outconv + head)
+// One block (1024 threads, one per CU) = 16 rows i0..i0+15 of slot b, all N columns.  Phases:
+//  1. outconv of the block's 16 rows and of row 0 (x0, needed by the trace update) into LDS:
+//     L lanes per pixel (L = C/4 up to 16), float4 channel loads, U pixels per lane group in
+//     flight, dot4_fma + xor-tree over the L lanes - the arithmetic of outconv_fwd_kernel (whose
+//     idle lanes add zeros), so X is bit-identical to the two-launch path;
+//  2. Weff_b = w + alpha (.) H_b in chunks of kc rows through LDS (all of it at N <= 128); Y = X Weff
+//     on v_mfma_f32_16x16x4_f32 (column tile t -> wave t mod 16) and y0 = x0 Weff as a VALU fmaf
+//     chain in the same k order (== the MFMA's, bitwise), so every block holds row 0's Y;
+//  3. Y = sigmoid, X rows written out (the backward's input);
+//  4. H'[k][j] for the block's rows k from H, x0[k], y0[j] (unet_p.py:81-86 operation order).
+constexpr int FH_R = 16;      // rows per block
+constexpr int FH_NT = 1024;   // threads per block
+constexpr int FH_LDS_W = 16384;   // floats of the Weff chunk (64 KB)
+
+template <typename T>
+__device__ __forceinline__ f32x4 fh_ld4(const T* p);
+template <>
+__device__ __forceinline__ f32x4 fh_ld4<float>(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+template <>
+__device__ __forceinline__ f32x4 fh_ld4<__bf16>(const __bf16* p) {
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    const b4 v = *reinterpret_cast<const b4*>(p);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+template <typename T, int L, int TPW>
+__global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ wo,
+                                                               const float* __restrict__ bo, int C,
+                                                               const float* __restrict__ H, const float* __restrict__ w,
+                                                               const float* __restrict__ alpha,
+                                                               const float* __restrict__ eta_p, float* __restrict__ X,
+                                                               float* __restrict__ Y, float* __restrict__ Hn, int N,
+                                                               FastDiv dN, int kc, int rule) {
+    extern __shared__ float fh_lds[];
+    float* xs = fh_lds;                       // [FH_R + 1][N]: own rows, then row 0
+    float* ws = xs + (FH_R + 1) * N;          // [kc][N]
+    float* y0s = ws + kc * N;                 // [N]
+    const int b = blockIdx.y;
+    const int i0 = blockIdx.x * FH_R;
+    const int tid = threadIdx.x;
+    const bool fuse = Hn != nullptr;
+    const long long nn = (long long)N * N;
+    const T* fb = feat + (long long)b * nn * C;
+    const float* Hb = H + (long long)b * nn;
+
+    // ---- 1. outconv
+    {
+        constexpr int U = L >= 8 ? 8 : 4;       // pixels per lane group in flight
+        const float bias = bo ? bo[0] : 0.f;
+        const int lane = tid % L;
+        constexpr int PPP = FH_NT / L;          // pixels per pass
+        const int npix = (fuse ? FH_R + 1 : FH_R) * N;
+        for (int q0 = tid / L; q0 < npix; q0 += U * PPP) {
+            const T* px[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = min(q0 + u * PPP, npix - 1);
+                const int r = (int)fdiv((unsigned)q, dN), k = q - r * N;
+                px[u] = fb + ((long long)(r < FH_R ? i0 + r : 0) * N + k) * C;
+            }
+            float s[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) s[u] = 0.f;
+            for (int c = lane * 4; c < C; c += 4 * L) {
+                const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + c);
+                f32x4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = fh_ld4<T>(px[u] + c);
+#pragma unroll
+                for (int u = 0; u < U; ++u) s[u] += dot4_fma(v[u], ww);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float t = s[u];
+                if (L >= 16) t += __shfl_xor(t, 8, 16);
+                if (L >= 8) t += __shfl_xor(t, 4, 16);
+                if (L >= 4) t += __shfl_xor(t, 2, 16);
+                if (L >= 2) t += __shfl_xor(t, 1, 16);
+                const int q = q0 + u * PPP;
+                if (lane == 0 && q < npix) xs[q] = t + bias;
+            }
+        }
+    }
+    __syncthreads();
+    // X rows of this block -> global (coalesced)
+    for (int e = tid; e < FH_R * N; e += FH_NT) X[(long long)b * nn + (long long)i0 * N + e] = xs[e];
+
+    // ---- 2. GEMM
+    const int wave = tid >> 6, l = tid & 63;
+    const int tiles = N / 16;
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float acc0 = 0.f;                                  // y0 chain of column tid (tid < N)
+    for (int k0 = 0; k0 < N; k0 += kc) {
+        {
+#pragma clang fp contract(off)
+            const int ne = kc * N;
+            for (int e0 = tid; e0 < ne; e0 += 8 * FH_NT) {
+                float wv[8], av[8], hv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const long long o = (long long)k0 * N + min(e0 + FH_NT * u, ne - 1);
+                    wv[u] = w[o]; av[u] = alpha[o]; hv[u] = Hb[o];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (e0 + FH_NT * u < ne) ws[e0 + FH_NT * u] = wv[u] + av[u] * hv[u];   // torch: w + mul(alpha, hebb)
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const int tile = wave + 16 * t;
+            if (tile < tiles) {
+                const float* wcol = ws + (l >> 4) * N + tile * 16 + (l & 15);
+                const float* xrow = xs + (l & 15) * N + k0 + (l >> 4);
+                for (int kk = 0; kk < kc; kk += 4)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xrow[kk], wcol[kk * N], acc[t], 0, 0, 0);
+            }
+        }
+        if (fuse && tid < N) {
+            float s0 = acc0;
+            for (int kk = 0; kk < kc; ++kk) s0 = fmaf(xs[FH_R * N + k0 + kk], ws[kk * N + tid], s0);
+            acc0 = s0;
+        }
+        __syncthreads();
+    }
+
+    // ---- 3. sigmoid + store (C layout of 16x16: column l & 15, rows 4 (l >> 4) + reg)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+        const int tile = wave + 16 * t;
+        if (tile < tiles) {
+            const int j = tile * 16 + (l & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int gi = i0 + 4 * (l >> 4) + r;
+                Y[((long long)b * N + gi) * N + j] = 1.f / (1.f + expf(-acc[t][r]));
+            }
+        }
+    }
+    if (!fuse) return;
+    if (tid < N) y0s[tid] = 1.f / (1.f + expf(-acc0));
+    __syncthreads();
+
+    // ---- 4. trace update of rows k = i0 .. i0+15
+    const float eta = eta_p[0];
+    const float one_m_eta = 1.f - eta;
+    float* Hnb = Hn + (long long)b * nn;
+    for (int e = tid; e < FH_R * N; e += FH_NT) {
+        const int kk = (int)fdiv((unsigned)e, dN), j = e - kk * N;
+        const long long o = (long long)(i0 + kk) * N + j;
+        Hnb[o] = trace_rule(Hb[o], xs[FH_R * N + i0 + kk], y0s[j], eta, one_m_eta, rule);
+    }
+}
+
 // ---------------------------------------------------------------------------------------- backward
 // G = dy * (1 - y) * y   (ATen sigmoid_backward: grad * (1 - out) * out)
 __device__ __forceinline__ float sig_bwd(float dy, float y) {
@@ -401,6 +560,50 @@ extern "C" int pu_plastic_fwd(const pu_plastic_args* a, void* stream) {
     int st = check_launch("pu_plastic_fwd");
     if (st != PU_OK || !a->hebb_out || fuse) return st;
     return pu_trace_update(a->hebb, a->x, a->y, a->eta, a->hebb_out, a->batch, a->nbf, a->rule, stream);
+}
+
+
+extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) {
+    PU_REQUIRE(a && a->feat && a->out_w && a->hebb && a->w && a->alpha && a->x && a->y && a->batch > 0,
+               "pu_plastic_head_fwd: bad args");
+    const int N = a->nbf, C = a->channels;
+    PU_REQUIRE(N >= 16 && N % 16 == 0 && N <= 512, "pu_plastic_head_fwd: nbf %d must be a multiple of 16 in [16, 512]", N);
+    PU_REQUIRE(C >= 4 && C % 4 == 0, "pu_plastic_head_fwd: channels %d must be a multiple of 4", C);
+    PU_REQUIRE((((uintptr_t)a->feat | (uintptr_t)a->out_w) & 15) == 0 || (a->feat_bf16 && ((uintptr_t)a->feat & 7) == 0 &&
+               ((uintptr_t)a->out_w & 15) == 0), "pu_plastic_head_fwd: feat / out_w alignment");
+    PU_REQUIRE(a->rule == PU_RULE_HEBB || a->rule == PU_RULE_OJA, "Must select one learning rule ('hebb' or 'oja')");
+    PU_REQUIRE(!a->hebb_out || (a->eta && a->hebb_out != a->hebb), "pu_plastic_head_fwd: hebb_out needs eta and no aliasing");
+    PU_REQUIRE((long long)N * N * C * a->batch < (1LL << 40), "pu_plastic_head_fwd: too large");
+    const int q = C / 4;
+    const int L = q >= 16 ? 16 : (q & (q - 1)) == 0 ? q : 16;    // lanes per pixel
+    const int kc = N * N <= FH_LDS_W ? N : FH_LDS_W / N;          // Weff rows per LDS chunk
+    const size_t lds = ((size_t)(FH_R + 1) * N + (size_t)kc * N + N) * sizeof(float);
+    const dim3 grid(N / FH_R, a->batch);
+    const FastDiv dN = make_fastdiv(N);
+    hipStream_t s = as_stream(stream);
+    const int tpw = (N / 16 + 15) / 16;                           // column tiles per wave (16 waves)
+#define PU_FH2(T_, L_, W_)                                                                                     \
+    hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat,     \
+                       a->out_w, a->out_b, C, a->hebb, a->w, a->alpha, a->eta, a->x, a->y, a->hebb_out, N, dN, kc, \
+                       a->rule)
+#define PU_FH(T_, L_)                                                                                       \
+    do {                                                                                                    \
+        if (tpw <= 1) PU_FH2(T_, L_, 1);                                                                    \
+        else PU_FH2(T_, L_, 2);                                                                             \
+    } while (0)
+#define PU_FH_L(T_)                                                                                         \
+    switch (L) {                                                                                            \
+        case 1: PU_FH(T_, 1); break;                                                                        \
+        case 2: PU_FH(T_, 2); break;                                                                        \
+        case 4: PU_FH(T_, 4); break;                                                                        \
+        case 8: PU_FH(T_, 8); break;                                                                        \
+        default: PU_FH(T_, 16); break;                                                                      \
+    }
+    if (a->feat_bf16) { PU_FH_L(__bf16) } else { PU_FH_L(float) }
+#undef PU_FH_L
+#undef PU_FH
+#undef PU_FH2
+    return check_launch("pu_plastic_head_fwd");
 }
 
 extern "C" size_t pu_plastic_bwd_workspace_bytes(int batch, int nbf) {

@@ -46,6 +46,12 @@ class PlasticArgs(ctypes.Structure):
                 ("y", P), ("hebb_out", P), ("rule", c_int)]
 
 
+class PlasticHeadArgs(ctypes.Structure):
+    _fields_ = [("batch", c_int), ("nbf", c_int), ("channels", c_int), ("feat", P), ("feat_bf16", c_int),
+                ("out_w", P), ("out_b", P), ("hebb", P), ("w", P), ("alpha", P), ("eta", P), ("x", P), ("y", P),
+                ("hebb_out", P), ("rule", c_int)]
+
+
 class PlasticBwdArgs(ctypes.Structure):
     _fields_ = [("batch", c_int), ("nbf", c_int), ("x", P), ("hebb", P), ("w", P), ("alpha", P), ("y", P),
                 ("dy", P), ("dx", P), ("dw", P), ("dalpha", P)]
@@ -99,6 +105,7 @@ SIGNATURES = [
     ("pu_outconv_workspace_bytes", c_size, [c_ll, c_int]),
     ("pu_outconv_bwd", c_int, [P, P, P, P, P, P, c_ll, c_int, c_int, P, c_size, P]),
     ("pu_plastic_fwd", c_int, [ctypes.POINTER(PlasticArgs), P]),
+    ("pu_plastic_head_fwd", c_int, [ctypes.POINTER(PlasticHeadArgs), P]),
     ("pu_trace_update", c_int, [P, P, P, P, P, c_int, c_int, c_int, P]),
     ("pu_plastic_bwd_workspace_bytes", c_size, [c_int, c_int]),
     ("pu_plastic_bwd", c_int, [ctypes.POINTER(PlasticBwdArgs), P, c_size, P]),

@@ -9,7 +9,7 @@ import os
 import torch
 
 from . import _lib
-from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticBwdArgs, AdamTensor, check,
+from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, check,
                    PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
@@ -407,6 +407,25 @@ def plastic_fwd(x, hebb, w, alpha, eta, rule, update_trace=True):
     with _Rec("plastic_fwd", flops=2.0 * B * N ** 3, nbytes=4.0 * (4 * B * N * N + 2 * N * N)):
         check(lib().pu_plastic_fwd(ctypes.byref(a), _stream()), "pu_plastic_fwd")
     return y, hn
+
+
+def plastic_head_fwd(feat, wo, bo, hebb, w, alpha, eta, rule, update_trace=True):
+    """The fused head (pu_plastic_head_fwd): feat [B,N,N,C] NHWC (fp32 / bf16), wo [C], bo [1] ->
+    (X [B,N,N] logits, Y [B,N,N], hebb' [B,N,N] or None)."""
+    dt = _act_dtype(feat)
+    _req(feat, "feat", dt)
+    for t, nm in ((wo, "wo"), (bo, "bo"), (hebb, "hebb"), (w, "w"), (alpha, "alpha"), (eta, "eta")):
+        _req(t, nm)
+    B, N, _, C = feat.shape
+    X = torch.empty(B, N, N, dtype=torch.float32, device=feat.device)
+    y = torch.empty_like(X)
+    hn = torch.empty_like(hebb) if update_trace else None
+    a = PlasticHeadArgs(B, N, C, feat.data_ptr(), int(dt == BF16), wo.data_ptr(), bo.data_ptr(), hebb.data_ptr(),
+                        w.data_ptr(), alpha.data_ptr(), eta.data_ptr(), X.data_ptr(), y.data_ptr(), _p(hn), rule)
+    nbytes = feat.element_size() * feat.numel() + 4.0 * (4 * B * N * N + 2 * N * N)
+    with _Rec("plastic_head_fwd", flops=2.0 * B * N ** 3 + 2.0 * B * N * N * C, nbytes=nbytes):
+        check(lib().pu_plastic_head_fwd(ctypes.byref(a), _stream()), "pu_plastic_head_fwd")
+    return X, y, hn
 
 
 def trace_update(hebb, x, y, eta, rule, out=None):

@@ -175,6 +175,7 @@ class ResTrunk:
         self.training = True
         self.gradbuf = None
         self.mask_fn = None      # (name, batch, channels, p) -> [B, C] scale; default: bernoulli
+        self.fused_head = False  # as UNetpTrunk.fused_head
         self.debug = None
 
     @staticmethod
@@ -289,6 +290,8 @@ class ResTrunk:
             y, st = self._stack_fwd(P, self.slots[name], u, src1)
             s[name] = st
         s["skips"] = skips
+        if self.fused_head:
+            return y, (s if save else None)
         o = self.slots["outc"]
         logits = K.outconv_fwd(y, P[o].reshape(-1), P[o + 1])
         return logits, (s if save else None)
@@ -356,12 +359,15 @@ class ResTrunk:
         skips = s["skips"]
         o = self.slots["outc"]
         y_last = s["uconv1"][6]
-        oo = out(o)
-        g, dwo, dbo = K.outconv_bwd(y_last, P[o].reshape(-1), dlogits, relu_mask=True,
-                                    out=None if oo is None else (oo[0].view(-1), oo[1]))
-        grads[o] = dwo.view_as(P[o])
-        grads[o + 1] = dbo
-        self._ready(o)
+        if self.fused_head:
+            g = dlogits                  # the fused head's outconv backward already applied the mask
+        else:
+            oo = out(o)
+            g, dwo, dbo = K.outconv_bwd(y_last, P[o].reshape(-1), dlogits, relu_mask=True,
+                                        out=None if oo is None else (oo[0].view(-1), oo[1]))
+            grads[o] = dwo.view_as(P[o])
+            grads[o + 1] = dbo
+            self._ready(o)
         gskip = [None] * 4
         for j in range(3, -1, -1):                       # uconv1 .. uconv4
             name = self.UP[j]

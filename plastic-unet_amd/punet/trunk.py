@@ -223,6 +223,9 @@ class UNetpTrunk:
             raise NotImplementedError("batch_norm / bilinear_upsample run in fp32 (precision='fp32')")
         self.gradbuf = None      # punet.dp.GradBuffer: backward writes grads into its views
         self.debug = None        # dict: when set, backward stores each layer's dZ (tests/diagnostics)
+        # True: forward returns the last activation (the outconv runs inside the fused head,
+        # punet.head.FusedHeadFunction) and backward receives dL/d(its pre-ReLU) from the head
+        self.fused_head = False
 
     def backward_order(self):
         """Parameters in the order backward() completes their gradients (outc first, stem last;
@@ -319,6 +322,8 @@ class UNetpTrunk:
             s["up%d.t" % j] = t
             y = self._conv("up%d.c1" % j, P, s, t)
             s["up%d.y" % j] = y
+        if self.fused_head:
+            return y, (s if save else None)
         o = self.slot["outc"]
         logits = K.outconv_fwd(y, P[o].reshape(-1), P[o + 1])
         return logits, (s if save else None)
@@ -350,12 +355,15 @@ class UNetpTrunk:
 
         y_last = s["up%d.y" % (D - 1)]
         outc = sl["outc"]
-        o = out(outc)
-        g, dwo, dbo = K.outconv_bwd(y_last, P[outc].reshape(-1), dlogits, relu_mask=True,
-                                    out=None if o is None else (o[0].view(-1), o[1]))
-        grads[outc] = dwo.view_as(P[outc])
-        grads[outc + 1] = dbo
-        self._ready(outc)
+        if self.fused_head:
+            g = dlogits                  # the fused head's outconv backward already applied the mask
+        else:
+            o = out(outc)
+            g, dwo, dbo = K.outconv_bwd(y_last, P[outc].reshape(-1), dlogits, relu_mask=True,
+                                        out=None if o is None else (o[0].view(-1), o[1]))
+            grads[outc] = dwo.view_as(P[outc])
+            grads[outc + 1] = dbo
+            self._ready(outc)
 
         gskip = [None] * (D - 1)
         for j in range(D - 1, 0, -1):
@@ -442,7 +450,8 @@ class UNetpTrunk:
 
 
 class TrunkFunction(torch.autograd.Function):
-    """autograd node: (trunk, save, x NCHW, *trunk params) -> logits [B,H,W]."""
+    """autograd node: (trunk, save, x NCHW, *trunk params) -> logits [B,H,W] (or, with
+    trunk.fused_head, the last activation [B,H,W,C] for the fused head)."""
 
     @staticmethod
     def forward(ctx, trunk, save, x, *params):

@@ -172,7 +172,15 @@ class UNetp(nn.Module):
         trunk.training = self.training      # BatchNorm: per-slot batch statistics vs running statistics
         params = trunk.params
         save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        from punet.head import fused_head_ok, FusedHeadFunction
+        wo, bo = self.outc.conv.weight, self.outc.conv.bias
+        trunk.fused_head = fused_head_ok(wo.shape[1], self.nbf, seq)
         logits = TrunkFunction.apply(trunk, save, x, *params)
+        if trunk.fused_head:
+            sink = None if trunk.gradbuf is None else (trunk.gradbuf, self.w, self.alpha, wo, bo)
+            Y, Hn = FusedHeadFunction.apply(logits, wo, bo, H, self.w, self.alpha, self.eta, RULES[self.rule], True,
+                                            sink)
+            return (Y[0], Hn[0]) if single else (Y, Hn)
         sink = None if trunk.gradbuf is None else (trunk.gradbuf, self.w, self.alpha)
         if seq:
             from punet.head import SequentialHeadFunction

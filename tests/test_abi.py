@@ -74,6 +74,7 @@ def test_header_structs_match_ctypes_layout():
     src = open(HEADER).read()
     for cname, py in [("pu_conv_args", _lib.ConvArgs), ("pu_wgrad_args", _lib.WgradArgs),
                       ("pu_plastic_args", _lib.PlasticArgs), ("pu_plastic_bwd_args", _lib.PlasticBwdArgs),
+                      ("pu_plastic_head_args", _lib.PlasticHeadArgs),
                       ("pu_adam_tensor", _lib.AdamTensor)]:
         body = dict((n, b) for b, n in re.findall(r"typedef struct \{([^}]*)\}\s*(\w+);", src))[cname]
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)

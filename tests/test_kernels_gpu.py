@@ -286,3 +286,29 @@ def test_fused_head_trace_equals_two_launch_path(B, N, rule):
     Yr, Hr = oracle.plastic_head(X.cpu(), H.cpu(), w.cpu(), al.cpu(), eta.cpu(), "hebb" if rule == 0 else "oja")
     assert_close(Y, Yr)
     assert_close(Hn, Hr)
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+@pytest.mark.parametrize("B,N,C,dt", [(3, 128, 64, torch.float32), (2, 32, 8, torch.float32),
+                                      (2, 64, 12, torch.float32), (1, 512, 8, torch.float32),
+                                      (2, 48, 128, torch.float32), (3, 128, 64, torch.bfloat16)])
+def test_fused_head_equals_outconv_then_head(rule, B, N, C, dt):
+    """pu_plastic_head_fwd (outconv + Weff GEMM on v_mfma_f32_16x16x4_f32 + sigmoid + trace update,
+    one launch) is bit-identical to the two-kernel path outconv_fwd -> plastic_fwd: the outconv sum
+    uses the same lane tree, and the f32 MFMA is a k-ordered fma chain like the VALU head."""
+    g = torch.Generator().manual_seed(N + C)
+    feat = torch.randn(B, N, N, C, generator=g).relu_().to(dt).to(DEV)
+    wo = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    bo = torch.randn(1, generator=g).to(DEV)
+    H = (0.2 * torch.randn(B, N, N, generator=g)).to(DEV)
+    w = (0.05 * torch.randn(N, N, generator=g)).to(DEV)
+    al = (0.05 * torch.rand(N, N, generator=g)).to(DEV)
+    eta = torch.tensor([0.0137], device=DEV)
+    X, Y, Hn = K.plastic_head_fwd(feat, wo, bo, H, w, al, eta, rule, True)
+    X2 = K.outconv_fwd(feat, wo, bo)
+    Y2, Hn2 = K.plastic_fwd(X2, H, w, al, eta, rule, True)
+    assert torch.equal(X, X2)
+    assert torch.equal(Y, Y2)
+    assert torch.equal(Hn, Hn2)
+    X3, Y3, Hn3 = K.plastic_head_fwd(feat, wo, bo, H, w, al, eta, rule, False)      # eval: no trace
+    assert Hn3 is None and torch.equal(Y3, Y) and torch.equal(X3, X)

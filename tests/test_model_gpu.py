@@ -224,3 +224,29 @@ def test_input_validation_matches_reference():
     net.rule = "bogus"
     with pytest.raises(ValueError, match="Must select one learning rule"):
         net(torch.zeros(1, 1, 32, 32, device=DEV), torch.zeros(32, 32, device=DEV))
+
+
+def test_fused_head_model_path_equals_unfused():
+    """UNetp with the outconv fused into the head (default) vs the two-launch path: bitwise the
+    same Y, H' and every gradient (the backward is the same kernels on bit-identical X)."""
+    import punet.head as ph
+    res = []
+    for fuse in (True, False):
+        ph.FUSE_OUTCONV = fuse
+        try:
+            torch.manual_seed(2)
+            net = UNetp(1, 1, DEV, rule="oja", nbf=64, depth=4, base_ch=16)
+            g = torch.Generator().manual_seed(6)
+            x = torch.rand(3, 1, 64, 64, generator=g).to(DEV)
+            t = (torch.rand(3, 64, 64, generator=g) > 0.5).float().to(DEV)
+            H = (0.05 * torch.randn(3, 64, 64, generator=g)).to(DEV)
+            y, hn = net(x, H)
+            bce_loss(y, t).backward()
+            res.append((y.detach(), hn.detach(), {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                                                  if p.grad is not None}))
+        finally:
+            ph.FUSE_OUTCONV = True
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert res[0][2].keys() == res[1][2].keys()
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
