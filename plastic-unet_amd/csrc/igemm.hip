@@ -710,6 +710,7 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
         // ring slot ts landed when only the younger slot's loads are pending
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const float* a = lds + (ts % NBUF) * STAGE;
         const float* wp = a + A_FL;
         f32x4 xa[FM], xb[FM];
@@ -963,6 +964,7 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_lean_kernel(const IgemmParam
             constexpr int u = decltype(uc)::value;
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
             __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
             const float* a = lds + (u % 3) * STAGE;
             const float* wp = a + A_FL;
             f32x4 xa[FM], xb[FM];

@@ -214,6 +214,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(const IgemmBf16Params p
         if (NBUF == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const __bf16* a = lds + (t % NBUF) * STAGE;
         const __bf16* b = a + BM * BK16;
         bf16x8 fa[2][FM], fb[2][FN];

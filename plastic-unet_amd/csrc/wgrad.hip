@@ -430,6 +430,7 @@ __global__ __launch_bounds__(NW * 64) void wgrad_dma_kernel(const WgradParams p)
     for (int t = 0; t < T; ++t) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBUF - 2) * G) : "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const float* ps = lds + (t % NBUF) * STAGE;
         const float* qs = ps + WG_BM * BN;
         if constexpr (X6) {
@@ -699,6 +700,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");     // s_barrier is no compiler fence: keep LDS reads behind it
     };
 
     if (T > 0) {
@@ -707,6 +709,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
         load(1);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");     // s_barrier is no compiler fence: keep LDS reads behind it
     }
     int t = 0;
     for (; t + 1 < T; t += 2) {
@@ -1202,6 +1205,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const WgradBf16Params p
     for (int t = 0; t < T; ++t) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         const char* pb = reinterpret_cast<const char*>(lds + (t % NBUF) * STAGE);
         const char* qb = pb + IMG * 2;
         wbf16x8 fa[2][2], fb[2][2];   // [kstep][frag]
@@ -1405,6 +1409,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Par
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     };
 
     if (NG > 0) {
@@ -1416,6 +1421,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Par
         for (int j = 0; j < SPB; ++j) load(SPB + j, j);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     }
     int g = 0;
     for (; g + 1 < NG; g += 2) {

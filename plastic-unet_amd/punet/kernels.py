@@ -237,6 +237,7 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     nbytes = L.pu_wgrad_workspace_bytes(ctypes.byref(a))
     if nbytes == 0:
         check(L.pu_wgrad(ctypes.byref(a), None, 0, _stream()), "pu_wgrad")
+        return
     ws = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=rows.device)
     if _PROF is None:
         check(L.pu_wgrad(ctypes.byref(a), ws.data_ptr(), nbytes, _stream()), "pu_wgrad")

@@ -56,6 +56,9 @@ CONV_CASES = [
     (1, 9, 13, 64, 0, 136),     # planes kernel: N not a tile multiple, ragged pixels, ragged k-tile
     (2, 16, 32, 64, 64, 128),   # halo-reuse wgrad: two sources, 2 x 2 channel tiles, image-row edges
     (1, 32, 16, 192, 0, 64),    # halo-reuse wgrad: 3 input-channel tiles, 16-wide rows (every stage at both edges)
+    (8, 64, 64, 64, 0, 64),     # halo2 wgrad (64-channel tile): 8 stages per split, the 3-deep raw ring wraps
+    (2, 32, 32, 128, 128, 128), # halo2 wgrad (128-channel tile): two sources, 2 input tiles
+    (1, 16, 48, 64, 128, 192),  # halo2 wgrad (64-channel tiles): 3 input x 3 output tiles, 3 stages per row
     (2, 37, 45, 16, 0, 16),     # small-channel direct kernels: several 16x32 tiles, ragged edges
     (1, 19, 70, 4, 4, 4),       # small-channel, two 4-channel sources, N = 4
 ]
