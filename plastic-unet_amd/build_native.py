@@ -1,9 +1,17 @@
 """Build libplastic_unet.so (gfx950) in-tree with hipcc.
 
-    python plastic-unet_amd/build_native.py [--force] [--jobs N]
+    python plastic-unet_amd/build_native.py [--force] [--jobs N] [--variant debug|asan_host]
 
 Objects go to plastic-unet_amd/build/, the library to plastic-unet_amd/lib/libplastic_unet.so
 (both git-ignored; the .so travels to the GPU box with the repo snapshot).
+
+Variants (sanitizers / debug):
+  debug      lib/libplastic_unet_debug.so: -DPU_DEBUG (every entry point synchronises after its
+             launches and reports asynchronous faults as its own error), -O2 -g
+  asan_host  lib/libplastic_unet_asan_host.so: the HOST half of every source (argument checks,
+             planning, workspace sizing, the C-ABI) with AddressSanitizer (-Xarch_host only: GPU
+             ASan is not available on this pool), device code at -O1 - for CPU tests of the
+             boundary under LD_PRELOAD of the clang ASan runtime
 """
 import argparse
 import concurrent.futures as cf
@@ -140,15 +148,56 @@ def build(force=False, jobs=None, verbose=True, defines=(), lib=None):
     return target
 
 
+ASAN_RT = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+
+
+def build_variant(kind, verbose=True):
+    """Build a sanitizer / debug variant library (see the module docstring); returns its path."""
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    if kind == "debug":
+        return build(defines=("PU_DEBUG=1",), lib=os.path.join(LIBDIR, "libplastic_unet_debug.so"), verbose=verbose)
+    if kind != "asan_host":
+        raise ValueError("variant must be 'debug' or 'asan_host'")
+    target = os.path.join(LIBDIR, "libplastic_unet_asan_host.so")
+    flags = ["-O1", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + INCLUDE,
+             "-I" + CSRC, "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+    def one(src):
+        obj = os.path.join(BUILD, os.path.basename(src) + ".asan_host.o")
+        deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(INCLUDE, "plastic_unet.h")]
+        if _newer(deps, obj):
+            r = subprocess.run([HIPCC] + flags + ["-c", src, "-o", obj], capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError("asan_host compile failed: %s\n%s" % (src, r.stderr))
+        return obj
+    with cf.ThreadPoolExecutor(min(8, len(srcs))) as ex:
+        objs = list(ex.map(one, srcs))
+    objs.append(_build_id_object(source_hash(("asan_host",)), ".asan_host"))
+    if _newer(objs, target):
+        r = subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-fsanitize=address", "-o", target] + objs,
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("asan_host link failed:\n%s" % r.stderr)
+    if verbose:
+        print("built", target)
+    return target
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("-D", dest="defines", action="append", default=[])
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--variant", default=None, choices=["debug", "asan_host"])
     a = ap.parse_args()
     try:
-        build(a.force, a.jobs, defines=a.defines, lib=a.lib)
+        if a.variant:
+            build_variant(a.variant)
+        else:
+            build(a.force, a.jobs, defines=a.defines, lib=a.lib)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

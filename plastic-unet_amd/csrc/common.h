@@ -21,9 +21,16 @@ inline int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+// PU_DEBUG builds (build_native.py --variant debug -> lib/libplastic_unet_debug.so) synchronise
+// after every launch, so an asynchronous fault is reported by the entry point that caused it
+// (the HIP_LAUNCH_BLOCKING / AMD_SERIALIZE_KERNEL discipline, per call instead of per process).
 inline int check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(PU_ERR_LAUNCH, "%s: %s", what, hipGetErrorString(e));
+#ifdef PU_DEBUG
+    e = hipDeviceSynchronize();
+    if (e != hipSuccess) return fail(PU_ERR_LAUNCH, "%s (PU_DEBUG synchronous check): %s", what, hipGetErrorString(e));
+#endif
     return PU_OK;
 }
 

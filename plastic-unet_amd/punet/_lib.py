@@ -1,14 +1,13 @@
 """ctypes binding of libplastic_unet.so (include/plastic_unet.h).
 
 The library is the product's only compute path: importing a kernel wrapper without it raises
-immediately - there is no CPU or eager-PyTorch fallback.  torch is imported first so the HIP
+immediately - there is no CPU or eager-PyTorch fallback.  load() imports torch first so the HIP
 runtime torch ships (libamdhip64.so.7) is the one the library binds to; our kernels then run on
-torch's streams and device memory.
+torch's streams and device memory (PU_NO_TORCH=1 skips that: the host-ASan test loads the library
+into a torch-free interpreter).
 """
 import ctypes
 import os
-
-import torch  # noqa: F401  (must load the HIP runtime before the library)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PLASTIC_UNET_LIB",
@@ -137,6 +136,8 @@ def load():
         raise LibraryMissing(
             "libplastic_unet.so not found at %s - build it with `python plastic-unet_amd/build_native.py` "
             "(the plastic U-Net path has no CPU fallback)" % LIB_PATH)
+    if not os.environ.get("PU_NO_TORCH"):
+        import torch  # noqa: F401  (loads the HIP runtime the library binds to, before the library)
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
