@@ -1170,6 +1170,59 @@ __global__ __launch_bounds__(256) void smallconv_kernel(const IgemmParams p) {
     }
 }
 
+
+// ---------------------------------------------------------------- single-channel stem (C = 1)
+// The first 3x3 conv (inc.c0: 1 -> N channels, unet_p.py:208-215) is a K = 9 GEMM: nothing for
+// an MFMA tile to do, the layer is the write of its N-channel output.  A block stages the 1-channel
+// halo of a 16 x 64 pixel tile in LDS; lanes work in groups of L = N/4 per pixel, each lane 4
+// output channels (36 weights in registers), so every wave-instruction of the shared float4
+// epilogue (bias, ReLU, masks, ...) stores 4 pixels x N channels contiguously.
+constexpr int ST_TH = 16, ST_TW = 64;
+
+template <int N>
+__global__ __launch_bounds__(256) void stem_conv_kernel(const IgemmParams p) {
+    constexpr int L = N / 4;                  // lanes per pixel
+    constexpr int PG = 256 / L;               // pixels per block pass
+    constexpr int HH = ST_TH + 2, HW = ST_TW + 2;
+    __shared__ float tile[HH * HW];
+    const int tiles_w = (p.Wo + ST_TW - 1) / ST_TW;
+    const int tiles_h = (p.Ho + ST_TH - 1) / ST_TH;
+    int blk = blockIdx.x;
+    const int txi = blk % tiles_w;
+    blk /= tiles_w;
+    const int tyi = blk % tiles_h;
+    const int b = blk / tiles_h;
+    const int y0 = tyi * ST_TH - 1, x0 = txi * ST_TW - 1;
+    const long long img = (long long)b * p.Hi * p.Wi;
+    for (int e = threadIdx.x; e < HH * HW; e += 256) {
+        const int hy = e / HW, hx = e - hy * HW;
+        const int gy = y0 + hy, gx = x0 + hx;
+        tile[e] = ((unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) ? p.src0[img + (long long)gy * p.Wi + gx]
+                                                                                  : 0.f;
+    }
+    const int lane_c = threadIdx.x % L;       // channels 4 lane_c .. 4 lane_c + 3
+    float w[9][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t][e] = p.wt[(long long)(4 * lane_c + e) * p.k_pad + t];
+    __syncthreads();
+    for (int q = threadIdx.x / L; q < ST_TH * ST_TW; q += PG) {
+        const int row = q / ST_TW, col = q - row * ST_TW;
+        const int oy = tyi * ST_TH + row, ox = txi * ST_TW + col;
+        if (oy >= p.Ho || ox >= p.Wo) continue;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const float a = tile[(row + t / 3) * HW + col + t % 3];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaf(a, w[t][e], v[e]);
+        }
+        const int m = (b * p.Ho + oy) * p.Wo + ox;
+        epi_store4(p, epi_row(p, m), 4 * lane_c, v);
+    }
+}
+
 // ------------------------------------------------------------------------------------------ host
 struct TileCfg {
     int bm, bn;
@@ -1300,6 +1353,15 @@ static bool small_conv_ok(const pu_conv_args* a) {
            (a->cgroup == 0 || a->cgroup >= C) && (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
 }
 
+// the single-channel stem: 3x3 / s1 / p1 (same size), C = 1, N in {32, 48, 64} (4-channel lane
+// groups that divide a wave), plain (non-SHUFFLE2) float4 epilogue
+static bool stem_conv_ok(const pu_conv_args* a) {
+    const int C = a->c0 + a->c1;
+    return C == 1 && a->c1 == 0 && (a->n == 32 || a->n == 64) && a->kh == 3 && a->kw == 3 && a->stride == 1 &&
+           a->pad == 1 && a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) &&
+           vec_epilogue(a) && (a->cgroup == 0 || a->cgroup >= C);
+}
+
 static bool uses_x6(const pu_conv_args* a) {
     return a->weight6 && choose_mode(a->c0, a->c1) == LOAD_CHUNK16 && !small_conv_ok(a);
 }
@@ -1370,6 +1432,13 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
 
     hipStream_t s = as_stream(stream);
     const int N = a->n;
+    if (stem_conv_ok(a)) {
+        p.ksplit = 1;
+        const dim3 sgrid((unsigned)(((a->out_w + ST_TW - 1) / ST_TW) * ((a->out_h + ST_TH - 1) / ST_TH) * a->batch));
+        if (N == 64) hipLaunchKernelGGL((stem_conv_kernel<64>), sgrid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((stem_conv_kernel<32>), sgrid, dim3(256), 0, s, p);
+        return check_launch("pu_conv_igemm (stem)");
+    }
     if (small_conv_ok(a)) {
         p.ksplit = 1;
         const dim3 sgrid((unsigned)(((a->out_w + SC_TW - 1) / SC_TW) * ((a->out_h + SC_TH - 1) / SC_TH) * a->batch));
@@ -1450,7 +1519,7 @@ extern "C" int pu_split_weight6(const float* packed, void* out, int n, int k_pad
 extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
     if (!a || a->batch <= 0 || a->out_h <= 0 || a->out_w <= 0 || a->n <= 0 || a->k_pad <= 0) return 0;
     const long long M = (long long)a->batch * a->out_h * a->out_w;
-    if (small_conv_ok(a)) return 0;
+    if (small_conv_ok(a) || stem_conv_ok(a)) return 0;
     int bm, bn, ks, tp;
     plan_tiles(a, M, &bm, &bn, &ks, &tp);
     return split_bytes(M, a->n, ks);
@@ -1463,6 +1532,13 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
     plan_tiles(a, M, bm, bn, &ks, &tp);
     *mode = choose_mode(a->c0, a->c1);
     if (uses_x6(a)) *mode = 4;   // 6-product bf16
+    if (stem_conv_ok(a)) {           // reported as mode 5 ("stem"), tile ST_TH x ST_TW pixels
+        *bm = ST_TH * ST_TW;
+        *bn = a->n;
+        *mode = 5;
+        if (ksplit) *ksplit = 1;
+        return PU_OK;
+    }
     if (small_conv_ok(a)) {          // reported as mode 3 ("direct"), tile SC_TH x SC_TW pixels
         *bm = SC_TH * SC_TW;
         *bn = a->n;

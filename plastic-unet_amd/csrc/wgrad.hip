@@ -745,6 +745,75 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     }
 }
 
+// ------------------------------------------------------- single-channel stem weight gradient
+// dW[n][tap] = sum_m dZ[m][n] x[m + tap] and db[n] = sum_m dZ[m][n] for the 1 -> N stem conv
+// (inc.c0): the layer is the read of dZ (N channels per pixel).  Blocks sweep 16 x 64 pixel tiles
+// (grid-stride) with the 1-channel halo staged in LDS; lanes in groups of N/4 per pixel, each lane
+// 4 output channels x (9 taps + bias) accumulators over its pixels (dZ float4 loads: a
+// wave-instruction reads 4 pixels x N channels contiguously); the block's groups are summed in
+// fixed order through LDS into slab row [block][n][0..9] and the fixed-order split reduction
+// finishes - deterministic like every other weight gradient.
+constexpr int SWS_TH = 16, SWS_TW = 64;
+
+template <int N>
+__global__ __launch_bounds__(256) void wgrad_stem_kernel(const WgradParams p) {
+    constexpr int L = N / 4, PG = 256 / L;
+    constexpr int HH = SWS_TH + 2, HW = SWS_TW + 2;
+    constexpr int RED = PG * 10 * N;
+    __shared__ __attribute__((aligned(16))) float smem[RED > HH * HW ? RED : HH * HW];
+    const int tid = threadIdx.x;
+    const int lane_c = tid % L, grp = tid / L;
+    float acc[10][4];
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[k][e] = 0.f;
+    const int ntiles = p.batch * p.tiles_h * p.tiles_w;
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int txi = t % p.tiles_w;
+        const int tyi = (t / p.tiles_w) % p.tiles_h;
+        const int b = t / (p.tiles_w * p.tiles_h);
+        const int y0 = tyi * SWS_TH - 1, x0 = txi * SWS_TW - 1;
+        const long long img = (long long)b * p.Hi * p.Wi;
+        __syncthreads();                       // the previous tile's readers are done
+        for (int e = tid; e < HH * HW; e += 256) {
+            const int hy = e / HW, hx = e - hy * HW;
+            const int gy = y0 + hy, gx = x0 + hx;
+            smem[e] = ((unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi)
+                          ? p.src0[img + (long long)gy * p.Wi + gx] : 0.f;
+        }
+        __syncthreads();
+        for (int q = grp; q < SWS_TH * SWS_TW; q += PG) {
+            const int row = q / SWS_TW, col = q - row * SWS_TW;
+            const int oy = tyi * SWS_TH + row, ox = txi * SWS_TW + col;
+            if (oy >= p.Ho || ox >= p.Wo) continue;
+            const long long m = ((long long)b * p.Ho + oy) * p.Wo + ox;
+            const f32x4 dz = *reinterpret_cast<const f32x4*>(p.P + m * N + 4 * lane_c);
+#pragma unroll
+            for (int t9 = 0; t9 < 9; ++t9) {
+                const float a = smem[(row + t9 / 3) * HW + col + t9 % 3];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[t9][e] = fmaf(a, dz[e], acc[t9][e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[9][e] += dz[e];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) smem[(grp * 10 + k) * N + 4 * lane_c + e] = acc[k][e];
+    __syncthreads();
+    float* slab = p.slab + (long long)blockIdx.x * p.Nr * p.Kcp;
+    for (int idx = tid; idx < 10 * N; idx += 256) {
+        const int k = idx / N, n = idx - k * N;
+        float v = 0.f;
+        for (int g = 0; g < PG; ++g) v += smem[(g * 10 + k) * N + n];
+        slab[(long long)n * p.Kcp + k] = v;   // k = tap (C = 1); k = 9 = K: the bias column
+    }
+}
+
 // ------------------------------------------------------------- small-channel weight gradient
 // 3x3/s1/p1 with C <= 16 input and N <= 16 output channels (configs C4/C5's 8/16-channel levels):
 // a GEMM with N, K this small wastes most of an MFMA tile, so each block sweeps 16 x 32 pixel
@@ -942,12 +1011,18 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
 
 struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
-    bool qvec, dma, small, halo;
+    bool qvec, dma, small, halo, stem;
     int tiles_w, tiles_h;
     size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
     size_t part_bytes() const { return G > 1 ? (size_t)G * Nr * Kcp * sizeof(double) : 0; }
     size_t ws_bytes() const { return ((slab_bytes() + 255) / 256) * 256 + part_bytes(); }
 };
+
+static bool stem_wgrad_ok(const pu_wgrad_args* a) {
+    return a->c0 == 1 && a->c1 == 0 && (a->n == 32 || a->n == 64) && a->kh == 3 && a->kw == 3 && a->stride == 1 &&
+           a->pad == 1 && a->in_h == a->out_h && a->in_w == a->out_w && a->bias_mode == 1 &&
+           ((uintptr_t)a->rows & 15) == 0;
+}
 
 static bool small_wgrad_ok(const pu_wgrad_args* a) {
     const int C = a->c0 + a->c1;
@@ -978,15 +1053,16 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->Kcp = (pl->Kc + 3) / 4 * 4;
     pl->qvec = (a->c0 % 4 == 0) && (a->c1 % 4 == 0);
     pl->small = small_wgrad_ok(a);
+    pl->stem = stem_wgrad_ok(a);
     pl->halo = false;
     if (pl->qvec) {
         PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0, "pu_wgrad: sources must be 16-byte aligned");
     }
     PU_REQUIRE(((uintptr_t)a->rows & 15) == 0, "pu_wgrad: rows must be 16-byte aligned");
     pl->dma = pl->qvec;
-    if (pl->small) {                   // direct small-channel kernel: one slab row block per block
-        pl->tiles_w = ceil_div(a->out_w, SW_TW);
-        pl->tiles_h = ceil_div(a->out_h, SW_TH);
+    if (pl->small || pl->stem) {       // direct kernels: one slab row block per block
+        pl->tiles_w = ceil_div(a->out_w, pl->stem ? SWS_TW : SW_TW);
+        pl->tiles_h = ceil_div(a->out_h, pl->stem ? SWS_TH : SW_TH);
         const long long ntiles = (long long)a->batch * pl->tiles_w * pl->tiles_h;
         pl->splits = (int)(ntiles < 1024 ? ntiles : 1024);
         pl->BN = a->n; pl->BK = pl->K; pl->gx = pl->gy = 1; pl->mps = 0; pl->dma = false;
@@ -1505,7 +1581,7 @@ static int plan_wgrad_bf16(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->Nr = a->n + (a->bias_mode == 2 ? 1 : 0);
     pl->Kc = pl->K + (a->bias_mode == 1 ? 1 : 0);
     pl->Kcp = (pl->Kc + 3) / 4 * 4;
-    pl->qvec = true; pl->dma = true; pl->small = false;
+    pl->qvec = true; pl->dma = true; pl->small = false; pl->stem = false;
     pl->halo = a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->out_h &&
                a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 && a->n % 64 == 0 &&
                a->bias_mode != 2 && M * pl->C < (1LL << 31);
@@ -1552,7 +1628,7 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
     if (st != PU_OK) return st;
     if (bn) *bn = pl.BN;
     if (bk) *bk = pl.BK;
-    if (qvec) *qvec = pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo kernel
+    if (qvec) *qvec = pl.stem ? 4 : pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo, 4: stem
     if (splits) *splits = pl.splits;
     return PU_OK;
 }
@@ -1583,6 +1659,13 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
     p.gx = pl.gx;
     p.gy = pl.gy;
     p.batch = a->batch; p.tiles_w = pl.tiles_w; p.tiles_h = pl.tiles_h;
+    if (pl.stem && (phase & 1)) {
+        if (a->n == 64) hipLaunchKernelGGL(wgrad_stem_kernel<64>, dim3(pl.splits), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(wgrad_stem_kernel<32>, dim3(pl.splits), dim3(256), 0, s, p);
+        st = check_launch("pu_wgrad (stem)");
+        if (st != PU_OK) return st;
+        phase &= ~1;
+    }
     if (pl.small && (phase & 1)) {
         const int C = pl.C, N = a->n;
         const dim3 sg(pl.splits);

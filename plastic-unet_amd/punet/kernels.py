@@ -23,7 +23,7 @@ def lib():
 
 # ------------------------------------------------------------------------------ launch profiler
 _PROF = None
-_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6"}
+_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem"}
 
 # fp32 GEMM arithmetic of the MFMA convolutions: "split6" (default) = each fp32 product as 6 exact
 # bf16 products on the bf16 MFMA pipe (pu_split_weight6 / pu_conv_args.weight6, fp32-accurate);
@@ -177,7 +177,7 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
     M = batch * out_hw[0] * out_hw[1]
     tag = "igemm<%dx%d,%s%s>" % (bm.value, bn.value, _MODES[mode.value], ",k%d" % ks.value if ks.value > 1 else "")
     nb = 0.0
-    if mode.value == 3:    # direct small-channel kernel: HBM-bound, report its algorithmic bytes
+    if mode.value in (3, 5):    # direct small-channel / stem kernels: HBM-bound, report algorithmic bytes
         per = (c0 + c1) + n * (1 + int(accum) + int(resid is not None)) + n0_mask(n, n0, mask0, mask1)
         nb = 4.0 * M * per
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1), nbytes=nb):
@@ -245,7 +245,7 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct", "halo")[qv.value])
+    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct", "halo", "stem")[qv.value])
     if a.math == 1 and qv.value in (1, 3):
         tag = tag[:-1] + ",x6>"
     # the GEMM and the split reduction timed apart (they are separate kernels in rocprof too)

@@ -43,6 +43,8 @@ def assert_close(got, ref, rtol=1e-4, atol_rel=1e-5):
 CONV_CASES = [
     # B, H, W, c0, c1, cout
     (2, 16, 16, 1, 0, 8),       # stem: scalar loader
+    (2, 40, 70, 1, 0, 64),      # single-channel stem kernel (N = 64): partial 16 x 64 tiles
+    (1, 17, 33, 1, 0, 32),      # single-channel stem kernel (N = 32), odd sizes
     (2, 12, 20, 8, 0, 16),      # vec4 loader, non-square
     (3, 16, 16, 64, 0, 64),     # chunk16 loader, 256x64 tile
     (2, 8, 8, 16, 16, 24),      # two sources (concat), N not a tile multiple
