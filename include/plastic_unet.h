@@ -366,7 +366,10 @@ int pu_bce_bwd(const float* y, const float* t, long long n, const float* grad_lo
  * Multi-tensor Adam (torch.optim.Adam, amsgrad=False, maximize=False):
  *   m = lerp(m, g, 1-beta1) ; v = v*beta2 + (1-beta2) g^2 ;
  *   p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)      (weight_decay adds wd*p to g first)
- * step_size = lr/(1-beta1^t) and bc2_sqrt = sqrt(1-beta2^t) are computed by the caller.
+ * step_size = lr/(1-beta1^t) and bc2_sqrt = sqrt(1-beta2^t) are computed by the caller.  The
+ * hyper-parameters are the optimizer's Python doubles: 1-beta1 and 1-beta2 are formed in double and
+ * then rounded to fp32, as ATen does with the Scalar arguments of lerp_/addcmul_ (forming 1-beta2
+ * from an fp32-rounded beta2 = 0.999 would be 1.3e-5 off).
  * ------------------------------------------------------------------------------------------- */
 typedef struct {
     float* param;
@@ -376,8 +379,8 @@ typedef struct {
     long long numel;
 } pu_adam_tensor;
 
-int pu_adam_multi(const pu_adam_tensor* tensors, int n_tensors, float beta1, float beta2, float eps,
-                  float weight_decay, float step_size, float bc2_sqrt, void* stream);
+int pu_adam_multi(const pu_adam_tensor* tensors, int n_tensors, double beta1, double beta2, double eps,
+                  double weight_decay, double step_size, double bc2_sqrt, void* stream);
 
 #ifdef __cplusplus
 }

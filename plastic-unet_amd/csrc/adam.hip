@@ -26,19 +26,19 @@ struct AdamBatch {
     int count;
 };
 
-__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float b1, float b2, float eps,
-                                          float wd, float step_size, float bc2s) {
+__device__ __forceinline__ float adam_one(float& p, float g, float& m, float& v, float omb1, float b2, float omb2,
+                                          float eps, float wd, float step_size, float bc2s) {
 #pragma clang fp contract(off)
     if (wd != 0.f) g = g + wd * p;
     // ATen lerp (weight < 0.5): self + weight * (end - self)
-    m = m + (1.f - b1) * (g - m);
-    v = v * b2 + (1.f - b2) * g * g;
+    m = m + omb1 * (g - m);
+    v = v * b2 + omb2 * g * g;
     const float denom = sqrtf(v) / bc2s + eps;
     p = p + (-step_size) * (m / denom);
     return p;
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(const AdamBatch batch, float b1, float b2, float eps, float wd,
+__global__ __launch_bounds__(256) void adam_kernel(const AdamBatch batch, float omb1, float b2, float omb2, float eps, float wd,
                                                    float step_size, float bc2s) {
     // locate this block's tensor (count <= 32: linear scan of the prefix table)
     int t = 0;
@@ -62,14 +62,14 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch batch, float 
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 float pe = p[e], me = m[e], ve = v[e];
-                adam_one(pe, g[e], me, ve, b1, b2, eps, wd, step_size, bc2s);
+                adam_one(pe, g[e], me, ve, omb1, b2, omb2, eps, wd, step_size, bc2s);
                 p[e] = pe; m[e] = me; v[e] = ve;
             }
             *reinterpret_cast<f32x4*>(P + i) = p;
             *reinterpret_cast<f32x4*>(M + i) = m;
             *reinterpret_cast<f32x4*>(V + i) = v;
         } else {
-            for (long long e = i; e < i + 4 && e < n; ++e) adam_one(P[e], G[e], M[e], V[e], b1, b2, eps, wd, step_size, bc2s);
+            for (long long e = i; e < i + 4 && e < n; ++e) adam_one(P[e], G[e], M[e], V[e], omb1, b2, omb2, eps, wd, step_size, bc2s);
         }
     }
 }
@@ -78,8 +78,8 @@ __global__ __launch_bounds__(256) void adam_kernel(const AdamBatch batch, float 
 
 using namespace pu;
 
-extern "C" int pu_adam_multi(const pu_adam_tensor* tensors, int n_tensors, float beta1, float beta2, float eps,
-                             float weight_decay, float step_size, float bc2_sqrt, void* stream) {
+extern "C" int pu_adam_multi(const pu_adam_tensor* tensors, int n_tensors, double beta1, double beta2, double eps,
+                             double weight_decay, double step_size, double bc2_sqrt, void* stream) {
     PU_REQUIRE(n_tensors >= 0 && (n_tensors == 0 || tensors), "pu_adam_multi: bad tensor list");
     int i = 0;
     while (i < n_tensors) {
@@ -98,8 +98,9 @@ extern "C" int pu_adam_multi(const pu_adam_tensor* tensors, int n_tensors, float
         }
         b.block_start[b.count] = blocks;
         if (b.count == 0) continue;
-        hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), b, beta1, beta2, eps, weight_decay,
-                           step_size, bc2_sqrt);
+        hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), b, (float)(1.0 - beta1),
+                           (float)beta2, (float)(1.0 - beta2), (float)eps, (float)weight_decay, (float)step_size,
+                           (float)bc2_sqrt);
         int st = check_launch("pu_adam_multi");
         if (st != PU_OK) return st;
     }

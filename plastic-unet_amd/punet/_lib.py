@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("PLASTIC_UNET_LIB",
                           os.path.join(os.path.dirname(HERE), "lib", "libplastic_unet.so"))
 
 c_int, c_ll, c_size, c_float, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
+c_double = ctypes.c_double
 P = ctypes.c_void_p
 
 PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID = 1, 2, 4, 8
@@ -116,8 +117,8 @@ SIGNATURES = [
     ("pu_bn_bwd", c_int, [P, P, P, P, P, P, P, P, c_int, c_ll, c_int, P, P, P, c_size, P]),
     ("pu_upsample_bilinear2x_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_upsample_bilinear2x_bwd", c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
-    ("pu_adam_multi", c_int, [ctypes.POINTER(AdamTensor), c_int, c_float, c_float, c_float, c_float, c_float,
-                              c_float, P]),
+    ("pu_adam_multi", c_int, [ctypes.POINTER(AdamTensor), c_int, c_double, c_double, c_double, c_double, c_double,
+                              c_double, P]),
 ]
 
 _lib = None

@@ -42,8 +42,11 @@ def init_from_env(backend=None, timeout_s=600):
 @torch.no_grad()
 def broadcast_params(module, src=0):
     if dist.is_initialized() and dist.get_world_size() > 1:
-        for t in list(module.parameters()) + list(module.buffers()):
+        ts = list(module.parameters()) + list(module.buffers())
+        for t in ts:
             dist.broadcast(t.data, src)
+        # collectives write in place without bumping version counters; packed-operand caches key on them
+        torch.autograd.graph.increment_version(ts)
 
 
 class GradBuffer:

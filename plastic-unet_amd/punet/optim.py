@@ -8,6 +8,7 @@ optimizer state_dicts move between the two.  StepLR (train.py:67) works unchange
 import math
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import kernels as K
 
@@ -52,4 +53,7 @@ class FusedAdam(torch.optim.Optimizer):
                 K.adam_multi([i[0] for i in items], [i[1] for i in items], [i[2] for i in items],
                              [i[3] for i in items], beta1, beta2, group["eps"], group["weight_decay"],
                              step_size, math.sqrt(bc2))
+                # the kernel writes through raw pointers: bump the version counters so every cache
+                # keyed on them (the trunk's packed / split GEMM operands) sees the new values
+                increment_version([i[0] for i in items])
         return loss

@@ -264,7 +264,18 @@ def test_fused_adam_matches_torch_adam():
             b.grad = gr.to(DEV)
         dev[2].grad = None      # a parameter without gradient is skipped (eta, S3)
         ref[2].grad = None
+        b_ref = [a.detach().clone() for a in ref]
+        b_dev = [b.detach().cpu() for b in dev]
         o1.step(); o2.step(); s1.step(); s2.step()
+        # each step's update to 1e-6 of its own size (+1 ulp of the parameter): 1-beta2 formed from an
+        # fp32-rounded beta2 (1.3e-5 off) fails this
+        for a, b, a0, b0 in zip(ref, dev, b_ref, b_dev):
+            assert torch.equal(a0, b0)
+            du_ref = (a.detach() - a0).double()
+            du_dev = (b.detach().cpu() - a0).double()
+            bound = 1e-6 * du_ref.abs().max().item() + 1.2e-7 * a0.abs().max().item()
+            assert (du_dev - du_ref).abs().max().item() <= bound, (step, a.shape)
+            b.data.copy_(a.detach())     # judge every step from the same parameters
     for a, b in zip(ref, dev):
         assert_close(b, a, rtol=1e-6, atol_rel=1e-6)
 

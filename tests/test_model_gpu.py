@@ -95,12 +95,12 @@ def test_c8_three_adam_steplr_steps_golden():
         errs.append((k, rel(sd[k].cpu(), sd64[k]), rel(_t(g["p." + k]), sd64[k])))
     for k, e_g, e_c in errs:
         print("%-36s gpu-fp64 %.2e   cpu32-fp64 %.2e (rel L2)" % (k, e_g, e_c))
-    # Adam's first steps move every coordinate by ~lr * g/(|g|+eps) with eps = 1e-8, so gradient
-    # coordinates near 0 (this net's deep-layer gradients are ~1e-8..1e-10) turn fp32 rounding
-    # and the occasional ReLU-branch flip (tests/test_precision_gpu.py) into O(lr) moves.  Bound
-    # the relative L2 deviation and require the same update direction almost everywhere.
+    # The GPU's deviation from the fp64 run must be of the CPU fp32 reference's own size (measured:
+    # within 1.5x for every tensor).  This bar caught two real defects that a looser one hid: packed
+    # conv weights not refreshed after FusedAdam (1e-4 of the fp64 run) and 1-beta2 formed from an
+    # fp32-rounded beta2 (1.3e-5 relative in v).
     for k, e_g, e_c in errs:
-        assert e_g <= max(16 * e_c, 5e-2), (k, e_g, e_c)
+        assert e_g <= 4 * e_c + 2e-7, (k, e_g, e_c)
     agree, total = 0, 0
     for k in sd:
         if k == "eta":
@@ -250,3 +250,100 @@ def test_fused_head_model_path_equals_unfused():
     assert res[0][2].keys() == res[1][2].keys()
     for k in res[0][2]:
         assert torch.equal(res[0][2][k], res[1][2][k]), k
+
+
+def test_teacher_forced_trajectory_step_by_step():
+    """The multi-step trajectory with the chaotic part removed: for 6 steps of the reference loop
+    (bs=1, trace carried, Adam + per-sample StepLR, train.py:91-112) the oracle is re-seeded with
+    the GPU's CURRENT parameters and trace at every step, so each step is judged on its own:
+      * loss within 1e-4 relative (north star) and Y / H' within 1e-4 of the fp64 oracle;
+      * the gradients at that point within 1e-4 aggregate relative L2 of fp64 (per tensor 2e-3:
+        an fp32 pre-activation within noise of 0 may take the other ReLU branch);
+      * the optimizer in isolation: FusedAdam's update of every parameter equals an fp64 Adam
+        applied to the SAME fp32 gradient and moments to 1e-6 relative, and the learning rate
+        follows StepLR exactly - a systematic optimizer bias cannot hide in trajectory noise."""
+    gi, g = golden("unetp_c8_init.npz"), golden("unetp_c8_adam.npz")
+    net = UNetp(1, 1, DEV, rule="oja", nbf=64)
+    load_prefixed(net, gi, "p.")
+    opt = FusedAdam(net.parameters(), lr=1e-3)
+    sch = torch.optim.lr_scheduler.StepLR(opt, gamma=0.666, step_size=2)
+    ref = oracle.RefUNetp(1, 1, rule="oja", nbf=64).double()
+    hebb = net.initialZeroHebb()
+    gen = torch.Generator().manual_seed(13)
+    moments = {}
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    for step in range(6):
+        x = torch.rand(1, 1, 64, 64, generator=gen)
+        t = (torch.rand(64, 64, generator=gen) > 0.5).float()
+        ref.load_state_dict({k: v.detach().cpu().double() for k, v in net.state_dict().items()})
+        ref.zero_grad(set_to_none=True)
+        yr, hr = ref(x.double(), hebb.detach().cpu().double())
+        lr_ = oracle.bce_loss(yr.reshape(-1), t.double().reshape(-1))
+        lr_.backward()
+        opt.zero_grad()
+        y, hn = net(x.to(DEV), hebb.detach())
+        loss = bce_loss(y.view(-1), t.to(DEV).view(-1))
+        loss.backward()
+        e_loss = abs(loss.item() - lr_.item()) / abs(lr_.item())
+        e_y = ((y.double().cpu() - yr).abs().max() / yr.abs().max()).item()
+        e_h = ((hn.double().cpu() - hr).abs().max() / max(hr.abs().max().item(), 1e-30)).item()
+        print("step %d: loss %.3g  Y %.3g  H' %.3g" % (step, e_loss, e_y, e_h), flush=True)
+        assert e_loss <= 1e-4, step
+        assert e_y < 1e-4, step
+        assert e_h < 1e-4, step
+        num = den = 0.0
+        for (k, p), (_, pr) in zip(net.named_parameters(), ref.named_parameters()):
+            if k == "eta":
+                assert p.grad is None and pr.grad is None
+                continue
+            d = (p.grad.double().cpu() - pr.grad).norm().item()
+            num, den = num + d * d, den + pr.grad.norm().item() ** 2
+            assert d <= 2e-3 * max(pr.grad.norm().item(), 1e-30), (step, k)
+        assert (num / den) ** 0.5 <= 1e-4, (step, (num / den) ** 0.5)
+        # the optimizer alone, on the GPU's own gradients
+        lr_now = opt.param_groups[0]["lr"]
+        assert lr_now == 1e-3 * 0.666 ** (step // 2)
+        before = {k: p.detach().double().cpu().clone() for k, p in net.named_parameters()}
+        grads = {k: p.grad.double().cpu().clone() for k, p in net.named_parameters() if p.grad is not None}
+        opt.step()
+        sch.step()
+        for k, p in net.named_parameters():
+            if k not in grads:
+                assert torch.equal(p.detach().double().cpu(), before[k])     # eta: no grad, untouched (S3)
+                continue
+            m, v = moments.get(k, (torch.zeros_like(grads[k]), torch.zeros_like(grads[k])))
+            m = b1 * m + (1 - b1) * grads[k]
+            v = b2 * v + (1 - b2) * grads[k] ** 2
+            moments[k] = (m, v)
+            n = step + 1
+            upd = lr_now * (m / (1 - b1 ** n)) / ((v / (1 - b2 ** n)).sqrt() + eps)
+            got = before[k] - p.detach().double().cpu()
+            scale = upd.abs().max().item()
+            err = (got - upd).abs()
+            i = int(err.argmax())
+            assert err.max().item() <= 1e-6 * max(scale, 1e-30) + 2e-7 * before[k].abs().max().item(), (
+                step, k, err.max().item(), scale, before[k].abs().max().item(), grads[k].reshape(-1)[i].item(),
+                m.reshape(-1)[i].item(), v.reshape(-1)[i].item(), upd.reshape(-1)[i].item(), got.reshape(-1)[i].item())
+        hebb = hn.detach()
+
+
+def test_forward_after_optimizer_step_sees_new_weights():
+    """FusedAdam writes parameters through raw pointers; the trunk caches packed / split GEMM
+    operands keyed on the parameter's version counter.  After opt.step() the next forward must be
+    bit-identical to a fresh model loaded with the updated state (no stale packed weights), and a
+    DP broadcast must invalidate the same way."""
+    torch.manual_seed(3)
+    net = UNetp(1, 1, DEV, rule="oja", nbf=64)
+    opt = FusedAdam(net.parameters(), lr=1e-2)
+    x = torch.rand(1, 1, 64, 64, device=DEV)
+    t = (torch.rand(64, 64, device=DEV) > 0.5).float()
+    h0 = net.initialZeroHebb()
+    y0, _ = net(x, h0)
+    bce_loss(y0.view(-1), t.view(-1)).backward()
+    opt.step()
+    y1, h1 = net(x, h0)
+    fresh = UNetp(1, 1, DEV, rule="oja", nbf=64)
+    fresh.load_state_dict(net.state_dict())
+    y2, h2 = fresh(x, h0)
+    assert not torch.equal(y1, y0)
+    assert torch.equal(y1, y2) and torch.equal(h1, h2)
