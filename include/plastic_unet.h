@@ -214,6 +214,19 @@ enum {
  * the K axis channel-group-major (see pu_conv_args.cgroup) for the FWD/DGRAD/CONVT_DGRAD modes. */
 int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw,
                    int k_pad, int cgroup, void* stream);
+/* Every packed GEMM operand of a model refreshed in one launch (after an optimizer step): job j
+ * packs w like pu_pack_weight(mode, cgroup) into any of packed (fp32 [rows][k_pad]), packed_bf16
+ * (bf16 [rows][k_pad]) and planes (the exact 3-term bf16 split of the fp32 packed operand,
+ * pu_split_weight6's [k_pad/16][6][rows][8]) - bit-identical to those calls.  k_pad a multiple of 8
+ * (16 with planes); outputs 16-byte aligned. */
+typedef struct {
+    const float* w;
+    float* packed;
+    void* packed_bf16;
+    void* planes;
+    int mode, d0, d1, kh, kw, k_pad, cgroup;
+} pu_pack_job;
+int pu_pack_weights(const pu_pack_job* jobs, int n_jobs, void* stream);
 int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, int h, int w, void* stream);
 
 /* Dropout2d application (unet_p_res.py:209,248) on NHWC: y[b][p][c] = x[b][p][c] * scale[b][c]

@@ -35,52 +35,114 @@ __device__ __forceinline__ int ungroup_k(int k, int C, int taps, int G) {
     return tap * C + g * G + cg;
 }
 
+// packed operand element (row, column kc of the packed K axis) of the parameter w (layouts: plastic_unet.h)
+__device__ __forceinline__ float pack_value(const float* __restrict__ w, int mode, int d0, int d1, int taps,
+                                            int row, int kc, int G) {
+    const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;   // channels along K (taps*Ck columns)
+    const int k = (mode == PU_PACK_CONVT_FWD) ? kc : ungroup_k(kc, Ck, taps, G);
+    float v = 0.f;
+    if (mode == PU_PACK_CONV_FWD) {          // w[O=d0][I=d1][R][S] -> [o][(r*S+s)*I+i]
+        if (k < taps * d1) {
+            int tap = k / d1, i = k - tap * d1;
+            v = w[((long long)row * d1 + i) * taps + tap];
+        }
+    } else if (mode == PU_PACK_CONV_DGRAD) { // -> [i][((R-1-r)*S+(S-1-s))*O+o]
+        if (k < taps * d0) {
+            int tapf = k / d0, o = k - tapf * d0;
+            int tap = taps - 1 - tapf;       // (R-1-r, S-1-s) flattened == taps-1-(r*S+s)
+            v = w[((long long)o * d1 + row) * taps + tap];
+        }
+    } else if (mode == PU_PACK_CONVT_FWD) {  // w[I=d0][O=d1][R][S] -> [(r*S+s)*O+o][i]
+        if (k < d0) {
+            int tap = row / d1, o = row - tap * d1;
+            v = w[((long long)k * d1 + o) * taps + tap];
+        }
+    } else if (mode == PU_PACK_CONVT_DGRAD) {  // -> [i][(r*S+s)*O+o]
+        if (k < taps * d1) {
+            int tap = k / d1, o = k - tap * d1;
+            v = w[((long long)row * d1 + o) * taps + tap];
+        }
+    } else {                                 // PU_PACK_CONVT3_FWD: w[I=d0][O=d1][3][3]
+        // row = (ph*2+pw)*O + o, k = (dh*2+dw)*I + i ; tap index along one axis: R(0,1)=0,
+        // R(0,0)=2, R(1,1)=1, R(1,0) = none
+        if (k < 4 * d0) {
+            const int phw = row / d1, o = row - phw * d1;
+            const int dhw = k / d0, i = k - dhw * d0;
+            const int ph = phw >> 1, pw = phw & 1, dh = dhw >> 1, dw = dhw & 1;
+            const int r = ph == 0 ? (dh ? 0 : 2) : (dh ? 1 : -1);
+            const int q = pw == 0 ? (dw ? 0 : 2) : (dw ? 1 : -1);
+            if (r >= 0 && q >= 0) v = w[(((long long)i * d1 + o) * 3 + r) * 3 + q];
+        }
+    }
+    return v;
+}
+
 template <typename TO>
 __global__ void pack_weight_kernel(const float* __restrict__ w, TO* __restrict__ p, int mode, int d0, int d1,
                                    int kh, int kw, int k_pad, int rows, int G) {
     const long long total = (long long)rows * k_pad;
     const int taps = kh * kw;
-    const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;   // channels along K (taps*Ck columns)
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * blockDim.x) {
         const int row = int(idx / k_pad);
-        const int k = (mode == PU_PACK_CONVT_FWD) ? int(idx - (long long)row * k_pad)
-                                                   : ungroup_k(int(idx - (long long)row * k_pad), Ck, taps, G);
-        float v = 0.f;
-        if (mode == PU_PACK_CONV_FWD) {          // w[O=d0][I=d1][R][S] -> [o][(r*S+s)*I+i]
-            if (k < taps * d1) {
-                int tap = k / d1, i = k - tap * d1;
-                v = w[((long long)row * d1 + i) * taps + tap];
-            }
-        } else if (mode == PU_PACK_CONV_DGRAD) { // -> [i][((R-1-r)*S+(S-1-s))*O+o]
-            if (k < taps * d0) {
-                int tapf = k / d0, o = k - tapf * d0;
-                int tap = taps - 1 - tapf;       // (R-1-r, S-1-s) flattened == taps-1-(r*S+s)
-                v = w[((long long)o * d1 + row) * taps + tap];
-            }
-        } else if (mode == PU_PACK_CONVT_FWD) {  // w[I=d0][O=d1][R][S] -> [(r*S+s)*O+o][i]
-            if (k < d0) {
-                int tap = row / d1, o = row - tap * d1;
-                v = w[((long long)k * d1 + o) * taps + tap];
-            }
-        } else if (mode == PU_PACK_CONVT_DGRAD) {  // -> [i][(r*S+s)*O+o]
-            if (k < taps * d1) {
-                int tap = k / d1, o = k - tap * d1;
-                v = w[((long long)row * d1 + o) * taps + tap];
-            }
-        } else {                                 // PU_PACK_CONVT3_FWD: w[I=d0][O=d1][3][3]
-            // row = (ph*2+pw)*O + o, k = (dh*2+dw)*I + i ; tap index along one axis: R(0,1)=0,
-            // R(0,0)=2, R(1,1)=1, R(1,0) = none
-            if (k < 4 * d0) {
-                const int phw = row / d1, o = row - phw * d1;
-                const int dhw = k / d0, i = k - dhw * d0;
-                const int ph = phw >> 1, pw = phw & 1, dh = dhw >> 1, dw = dhw & 1;
-                const int r = ph == 0 ? (dh ? 0 : 2) : (dh ? 1 : -1);
-                const int q = pw == 0 ? (dw ? 0 : 2) : (dw ? 1 : -1);
-                if (r >= 0 && q >= 0) v = w[(((long long)i * d1 + o) * 3 + r) * 3 + q];
-            }
+        p[idx] = (TO)pack_value(w, mode, d0, d1, taps, row, int(idx - (long long)row * k_pad), G);
+    }
+}
+
+// Every packed operand of a model in one launch (pu_pack_weights): a lane produces 8 consecutive K
+// columns of one row -> the fp32 packed row (2 x 16 B), the bf16 packed row (16 B) and/or the three
+// exact bf16 split planes (3 x 16 B, [k_pad/16][6][rows][8], the split of split_weight6_kernel).
+constexpr int PACK_MAX_JOBS = 32;
+struct PackBatch {
+    const float* w[PACK_MAX_JOBS];
+    float* packed[PACK_MAX_JOBS];
+    __bf16* packed_bf16[PACK_MAX_JOBS];
+    __bf16* planes[PACK_MAX_JOBS];
+    int mode[PACK_MAX_JOBS], d0[PACK_MAX_JOBS], d1[PACK_MAX_JOBS], taps[PACK_MAX_JOBS];
+    int rows[PACK_MAX_JOBS], k_pad[PACK_MAX_JOBS], G[PACK_MAX_JOBS];
+    int block_start[PACK_MAX_JOBS + 1];
+    int count;
+};
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(256) void pack_multi_kernel(const PackBatch b) {
+#pragma clang fp contract(off)
+    int j = 0;
+    while (j + 1 < b.count && (int)blockIdx.x >= b.block_start[j + 1]) ++j;
+    const int k_pad = b.k_pad[j], rows = b.rows[j];
+    const int chunks = k_pad >> 3;
+    const long long c = (long long)(blockIdx.x - b.block_start[j]) * 256 + threadIdx.x;
+    if (c >= (long long)rows * chunks) return;
+    const int row = (int)(c / chunks);
+    const int k0 = (int)(c - (long long)row * chunks) * 8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = pack_value(b.w[j], b.mode[j], b.d0[j], b.d1[j], b.taps[j], row, k0 + e, b.G[j]);
+    const long long o = (long long)row * k_pad + k0;
+    if (b.packed[j]) {
+        *reinterpret_cast<f32x4*>(b.packed[j] + o) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(b.packed[j] + o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+    if (b.packed_bf16[j]) {
+        bf16x8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) h[e] = (__bf16)v[e];
+        *reinterpret_cast<bf16x8*>(b.packed_bf16[j] + o) = h;
+    }
+    if (b.planes[j]) {
+        bf16x8 hi, mid, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const __bf16 a = (__bf16)v[e];
+            const float r = v[e] - (float)a;
+            const __bf16 m = (__bf16)r;
+            hi[e] = a; mid[e] = m; lo[e] = (__bf16)(r - (float)m);
         }
-        p[idx] = (TO)v;
+        const int t = k0 >> 4, half = (k0 >> 3) & 1;
+        __bf16* P = b.planes[j];
+        *reinterpret_cast<bf16x8*>(P + (((long long)t * 6 + 0 + half) * rows + row) * 8) = hi;
+        *reinterpret_cast<bf16x8*>(P + (((long long)t * 6 + 2 + half) * rows + row) * 8) = mid;
+        *reinterpret_cast<bf16x8*>(P + (((long long)t * 6 + 4 + half) * rows + row) * 8) = lo;
     }
 }
 
@@ -449,10 +511,10 @@ __global__ void bf16_to_f32_kernel(const __bf16* __restrict__ x, float* __restri
 
 using namespace pu;
 
-template <typename TO>
-static int pack_weight_impl(const float* w, TO* packed, int mode, int d0, int d1, int kh, int kw, int k_pad, int cgroup,
-                            void* stream, const char* name) {
-    PU_REQUIRE(w && packed && d0 > 0 && d1 > 0 && kh > 0 && kw > 0 && k_pad > 0, "%s: bad args", name);
+// argument checks shared by the pack entry points; *rows = rows of the packed operand
+static int pack_check(const float* w, int mode, int d0, int d1, int kh, int kw, int k_pad, int cgroup, int* rows,
+                      const char* name) {
+    PU_REQUIRE(w && d0 > 0 && d1 > 0 && kh > 0 && kw > 0 && k_pad > 0, "%s: bad args", name);
     PU_REQUIRE(cgroup == 0 || cgroup == 16 || cgroup == 32, "%s: cgroup %d", name, cgroup);
     if (cgroup) {
         const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;
@@ -461,19 +523,62 @@ static int pack_weight_impl(const float* w, TO* packed, int mode, int d0, int d1
     PU_REQUIRE(mode >= 0 && mode <= 4, "%s: mode %d", name, mode);
     PU_REQUIRE(mode != PU_PACK_CONVT3_FWD || (kh == 3 && kw == 3 && cgroup == 0), "%s: CONVT3_FWD is 3x3, tap-major", name);
     const int taps = kh * kw;
-    int rows, kmin;
+    int kmin;
     switch (mode) {
-        case PU_PACK_CONV_FWD: rows = d0; kmin = taps * d1; break;
-        case PU_PACK_CONV_DGRAD: rows = d1; kmin = taps * d0; break;
-        case PU_PACK_CONVT_FWD: rows = taps * d1; kmin = d0; break;
-        case PU_PACK_CONVT3_FWD: rows = 4 * d1; kmin = 4 * d0; break;
-        default: rows = d0; kmin = taps * d1; break;
+        case PU_PACK_CONV_FWD: *rows = d0; kmin = taps * d1; break;
+        case PU_PACK_CONV_DGRAD: *rows = d1; kmin = taps * d0; break;
+        case PU_PACK_CONVT_FWD: *rows = taps * d1; kmin = d0; break;
+        case PU_PACK_CONVT3_FWD: *rows = 4 * d1; kmin = 4 * d0; break;
+        default: *rows = d0; kmin = taps * d1; break;
     }
     PU_REQUIRE(k_pad >= kmin, "%s: k_pad %d < %d", name, k_pad, kmin);
+    return PU_OK;
+}
+
+template <typename TO>
+static int pack_weight_impl(const float* w, TO* packed, int mode, int d0, int d1, int kh, int kw, int k_pad, int cgroup,
+                            void* stream, const char* name) {
+    PU_REQUIRE(packed, "%s: bad args", name);
+    int rows = 0;
+    const int st = pack_check(w, mode, d0, d1, kh, kw, k_pad, cgroup, &rows, name);
+    if (st != PU_OK) return st;
     const long long total = (long long)rows * k_pad;
     hipLaunchKernelGGL(pack_weight_kernel<TO>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), w, packed, mode,
                        d0, d1, kh, kw, k_pad, rows, cgroup);
     return check_launch(name);
+}
+
+extern "C" int pu_pack_weights(const pu_pack_job* jobs, int n_jobs, void* stream) {
+    PU_REQUIRE(n_jobs >= 0 && (n_jobs == 0 || jobs), "pu_pack_weights: bad job list");
+    int i = 0;
+    while (i < n_jobs) {
+        PackBatch b;
+        b.count = 0;
+        int blocks = 0;
+        while (i < n_jobs && b.count < PACK_MAX_JOBS) {
+            const pu_pack_job& J = jobs[i++];
+            int rows = 0;
+            const int st = pack_check(J.w, J.mode, J.d0, J.d1, J.kh, J.kw, J.k_pad, J.cgroup, &rows, "pu_pack_weights");
+            if (st != PU_OK) return st;
+            PU_REQUIRE(J.packed || J.packed_bf16 || J.planes, "pu_pack_weights: job %d has no output", i - 1);
+            PU_REQUIRE(J.k_pad % (J.planes ? 16 : 8) == 0, "pu_pack_weights: job %d k_pad %d", i - 1, J.k_pad);
+            PU_REQUIRE(((((uintptr_t)J.packed) | ((uintptr_t)J.packed_bf16) | ((uintptr_t)J.planes)) & 15) == 0,
+                       "pu_pack_weights: job %d outputs must be 16-byte aligned", i - 1);
+            const int k = b.count;
+            b.w[k] = J.w; b.packed[k] = J.packed; b.packed_bf16[k] = (__bf16*)J.packed_bf16; b.planes[k] = (__bf16*)J.planes;
+            b.mode[k] = J.mode; b.d0[k] = J.d0; b.d1[k] = J.d1; b.taps[k] = J.kh * J.kw;
+            b.rows[k] = rows; b.k_pad[k] = J.k_pad; b.G[k] = J.cgroup;
+            b.block_start[k] = blocks;
+            blocks += (int)(((long long)rows * (J.k_pad / 8) + 255) / 256);
+            b.count++;
+        }
+        b.block_start[b.count] = blocks;
+        if (b.count == 0) continue;
+        hipLaunchKernelGGL(pack_multi_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), b);
+        const int st = check_launch("pu_pack_weights");
+        if (st != PU_OK) return st;
+    }
+    return PU_OK;
 }
 
 extern "C" int pu_pack_weight(const float* w, float* packed, int mode, int d0, int d1, int kh, int kw, int k_pad,

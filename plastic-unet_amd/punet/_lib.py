@@ -61,6 +61,11 @@ class AdamTensor(ctypes.Structure):
     _fields_ = [("param", P), ("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("numel", c_ll)]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", P), ("packed", P), ("packed_bf16", P), ("planes", P), ("mode", c_int), ("d0", c_int),
+                ("d1", c_int), ("kh", c_int), ("kw", c_int), ("k_pad", c_int), ("cgroup", c_int)]
+
+
 # every symbol declared in include/plastic_unet.h: (name, restype, argtypes)
 SIGNATURES = [
     ("pu_abi_version", c_int, []),
@@ -117,6 +122,7 @@ SIGNATURES = [
     ("pu_bn_bwd", c_int, [P, P, P, P, P, P, P, P, c_int, c_ll, c_int, P, P, P, c_size, P]),
     ("pu_upsample_bilinear2x_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_upsample_bilinear2x_bwd", c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    ("pu_pack_weights", c_int, [ctypes.POINTER(PackJob), c_int, P]),
     ("pu_adam_multi", c_int, [ctypes.POINTER(AdamTensor), c_int, c_double, c_double, c_double, c_double, c_double,
                               c_double, P]),
 ]

@@ -9,12 +9,12 @@ import os
 import torch
 
 from . import _lib
-from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, check,
+from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, check,
                    PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
-           "bce_bwd", "adam_multi", "round16", "cgroup_for", "device_info", "lib"]
+           "bce_bwd", "adam_multi", "pack_weights", "round16", "cgroup_for", "device_info", "lib"]
 
 
 def lib():
@@ -268,7 +268,28 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
         check(fn(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, cgroup, _stream()), "pu_pack_weight")
     if out.dtype == torch.float32 and _FP32_MATH == "split6" and k_pad % 16 == 0:
         out._split6 = split_weight6(out)      # travels with the packed operand (igemm picks it up)
+    out._pack_spec = (mode, k_pad, cgroup)    # pack_weights() refreshes it in place
     return out
+
+
+def pack_weights(jobs):
+    """Refresh many packed operands in one launch (pu_pack_weights).  jobs: (w, packed, planes) with
+    ``packed`` an output of pack_weight (fp32 or bf16; its mode / k_pad / cgroup are read from the
+    attributes pack_weight stored on it) and ``planes`` its split6 planes or None."""
+    if not jobs:
+        return
+    arr = (PackJob * len(jobs))()
+    nbytes = 0.0
+    for i, (w, packed, planes) in enumerate(jobs):
+        _req(w, "w")
+        mode, k_pad, cg = packed._pack_spec
+        d0, d1, kh, kw = w.shape
+        bf = packed.dtype == BF16
+        arr[i] = PackJob(w.data_ptr(), None if bf else packed.data_ptr(), packed.data_ptr() if bf else None,
+                         None if planes is None else planes.data_ptr(), mode, d0, d1, kh, kw, k_pad, cg)
+        nbytes += 4.0 * w.numel() + packed.element_size() * packed.numel() + (0 if planes is None else 2.0 * planes.numel())
+    with _Rec("pack_weight", nbytes=nbytes):
+        check(lib().pu_pack_weights(arr, len(jobs), _stream()), "pu_pack_weights")
 
 
 def split_weight6(packed):

@@ -251,6 +251,7 @@ class ResTrunk:
 
     def forward(self, x, params, save, training):
         self.training = training       # BatchNorm: per-slot batch statistics vs running statistics
+        self.packs.refresh()           # operands of parameters the optimizer moved: one launch
         P = list(params)
         p_drop = self.model.dropout_ratio
         drop = training and p_drop > 0

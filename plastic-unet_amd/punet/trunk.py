@@ -25,7 +25,12 @@ from ._lib import PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PA
 
 
 class _Packs:
-    """Packed GEMM operands of the OIHW parameters, rebuilt only when a parameter changes."""
+    """Packed GEMM operands of the OIHW parameters, rebuilt only when a parameter changes.
+
+    The cache keys on the parameter's storage and checks its version counter (the optimizer and
+    the DP broadcast bump it).  ``refresh()`` - called once at the start of every trunk forward -
+    re-packs every stale entry in place with ONE multi-tensor launch (pu_pack_weights: pack + exact
+    bf16 split fused) instead of two launches per operand at first use."""
 
     def __init__(self):
         self.cache = {}
@@ -35,11 +40,19 @@ class _Packs:
         key = (w.data_ptr(), tuple(w.shape), mode, cgroup, dtype)
         ver = w._version
         hit = self.cache.get(key)
-        if hit is not None and hit[0] == ver:
+        if hit is not None and hit[0] == ver and hit[1]._pack_spec[1] == k_pad:
             return hit[1]
         packed = K.pack_weight(w.detach(), mode, k_pad, cgroup=cgroup, dtype=dtype)
-        self.cache[key] = (ver, packed)
+        self.cache[key] = (ver, packed, w)
         return packed
+
+    def refresh(self):
+        stale = [(key, w, packed) for key, (ver, packed, w) in self.cache.items()
+                 if w._version != ver and w.data_ptr() == key[0]]
+        if stale:
+            K.pack_weights([(w.detach(), packed, getattr(packed, "_split6", None)) for _, w, packed in stale])
+            for key, w, packed in stale:
+                self.cache[key] = (w._version, packed, w)
 
 
 def _kp(k, dt):
@@ -284,6 +297,7 @@ class UNetpTrunk:
         P = params
         D = self.depth
         pk = self.packs
+        pk.refresh()                   # operands of parameters the optimizer moved: one launch
         s = {"x": x}
         if self.coord is not None:     # stem: 1x1 conv + ReLU over the AddCoords input
             ci = self.slot["coord"]

@@ -75,7 +75,7 @@ def test_header_structs_match_ctypes_layout():
     for cname, py in [("pu_conv_args", _lib.ConvArgs), ("pu_wgrad_args", _lib.WgradArgs),
                       ("pu_plastic_args", _lib.PlasticArgs), ("pu_plastic_bwd_args", _lib.PlasticBwdArgs),
                       ("pu_plastic_head_args", _lib.PlasticHeadArgs),
-                      ("pu_adam_tensor", _lib.AdamTensor)]:
+                      ("pu_adam_tensor", _lib.AdamTensor), ("pu_pack_job", _lib.PackJob)]:
         body = dict((n, b) for b, n in re.findall(r"typedef struct \{([^}]*)\}\s*(\w+);", src))[cname]
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = []

@@ -328,3 +328,50 @@ def test_fused_head_equals_outconv_then_head(rule, B, N, C, dt):
     assert torch.equal(Hn, Hn2)
     X3, Y3, Hn3 = K.plastic_head_fwd(feat, wo, bo, H, w, al, eta, rule, False)      # eval: no trace
     assert Hn3 is None and torch.equal(Y3, Y) and torch.equal(X3, X)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_pack_weights_multi_equals_single_packs(dt):
+    """pu_pack_weights (every operand of a model, pack + exact bf16 split fused, one launch) is
+    bit-identical to pu_pack_weight (+ pu_split_weight6) per operand, for all five layouts, ragged
+    K padding and channel-group-major K."""
+    from punet._lib import PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD
+    g = torch.Generator().manual_seed(5)
+    specs = [((64, 32, 3, 3), PU_PACK_CONV_FWD, 32), ((64, 32, 3, 3), PU_PACK_CONV_DGRAD, 32),
+             ((24, 8, 3, 3), PU_PACK_CONV_FWD, 0), ((8, 1, 3, 3), PU_PACK_CONV_FWD, 0),
+             ((48, 64, 2, 2), PU_PACK_CONVT_FWD, 0), ((48, 64, 2, 2), PU_PACK_CONVT_DGRAD, 16),
+             ((40, 40, 3, 3), 4, 0), ((128, 96, 3, 3), PU_PACK_CONV_DGRAD, 32)] * 5   # > 32 jobs: 2 batches
+    jobs, refs = [], []
+    for shape, mode, cg in specs:
+        if dt == torch.bfloat16 and cg == 16:
+            cg = 32 if shape[1] % 32 == 0 else 0
+        w = (torch.randn(*shape, generator=g) * 3).to(DEV)
+        d0, d1, kh, kw = shape
+        kmin = {0: kh * kw * d1, 1: kh * kw * d0, 2: d0, 3: kh * kw * d1, 4: 4 * d0}[mode]
+        k_pad = (kmin + 31) // 32 * 32 if dt == torch.bfloat16 else K.round16(kmin)
+        ref = K.pack_weight(w, mode, k_pad, cgroup=cg, dtype=dt)
+        out = K.pack_weight(torch.zeros_like(w), mode, k_pad, cgroup=cg, dtype=dt)   # same buffers, zero content
+        jobs.append((w, out, getattr(out, "_split6", None)))
+        refs.append(ref)
+    K.pack_weights(jobs)
+    for (w, out, planes), ref in zip(jobs, refs):
+        assert torch.equal(out, ref)
+        if planes is not None:
+            assert torch.equal(planes, ref._split6)
+
+
+def test_pack_refresh_after_optimizer_is_one_launch():
+    """The trunk re-packs every moved parameter at the next forward in one pu_pack_weights call."""
+    from unet import UNetp
+    torch.manual_seed(0)
+    net = UNetp(1, 1, DEV, rule="oja", nbf=64)
+    x = torch.rand(1, 1, 64, 64, device=DEV)
+    h = net.initialZeroHebb()
+    y, _ = net(x, h)
+    y.sum().backward()
+    opt = FusedAdam(net.parameters(), lr=1e-3)
+    opt.step()
+    with K.KernelProfiler() as prof:
+        net(x, h)
+    s = prof.summary()
+    assert s["pack_weight"]["launches"] == 1, s.get("pack_weight")
