@@ -111,13 +111,47 @@ __global__ __launch_bounds__(256) void pack_multi_kernel(const PackBatch b) {
     while (j + 1 < b.count && (int)blockIdx.x >= b.block_start[j + 1]) ++j;
     const int k_pad = b.k_pad[j], rows = b.rows[j];
     const int chunks = k_pad >> 3;
-    const long long c = (long long)(blockIdx.x - b.block_start[j]) * 256 + threadIdx.x;
-    if (c >= (long long)rows * chunks) return;
-    const int row = (int)(c / chunks);
-    const int k0 = (int)(c - (long long)row * chunks) * 8;
+    // a wave covers 8 rows x 8 column chunks (64 columns): the fp32 rows are written as 256 B runs
+    // and each (t, half) plane segment as 8 rows x 16 B = one 128 B run
+    const int cgs = (chunks + 7) >> 3;
+    const long long wv = (long long)(blockIdx.x - b.block_start[j]) * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long long rg = wv / cgs;
+    const int row = (int)(rg * 8 + (lane >> 3));
+    const int chunk = (int)(wv - rg * cgs) * 8 + (lane & 7);
+    if (row >= rows || chunk >= chunks) return;
+    const int k0 = chunk * 8;
+    const int mode = b.mode[j], d0 = b.d0[j], d1 = b.d1[j], taps = b.taps[j], G = b.G[j];
+    const float* __restrict__ w = b.w[j];
     float v[8];
+    // fast path: the 8 columns are 8 consecutive channels of one tap -> one index decomposition and
+    // a constant source stride (no per-element integer divisions)
+    const int Ck = (mode == PU_PACK_CONV_DGRAD) ? d0 : d1;
+    long long base = -1, stride = 0;
+    if (mode == PU_PACK_CONVT_FWD) {
+        if (k0 + 8 <= d0) {
+            const int tap = row / d1, o = row - tap * d1;
+            base = ((long long)k0 * d1 + o) * taps + tap;
+            stride = (long long)d1 * taps;
+        }
+    } else if (mode != PU_PACK_CONVT3_FWD && Ck % 8 == 0 && (G == 0 || G % 8 == 0) && k0 + 8 <= taps * Ck) {
+        const int kk = ungroup_k(k0, Ck, taps, G);
+        const int tap = kk / Ck, c0 = kk - tap * Ck;
+        if (mode == PU_PACK_CONV_DGRAD) {
+            base = ((long long)c0 * d1 + row) * taps + (taps - 1 - tap);
+            stride = (long long)d1 * taps;
+        } else {   // CONV_FWD, CONVT_DGRAD: w[row][c][tap]
+            base = ((long long)row * d1 + c0) * taps + tap;
+            stride = taps;
+        }
+    }
+    if (base >= 0) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = pack_value(b.w[j], b.mode[j], b.d0[j], b.d1[j], b.taps[j], row, k0 + e, b.G[j]);
+        for (int e = 0; e < 8; ++e) v[e] = w[base + e * stride];
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = pack_value(w, mode, d0, d1, taps, row, k0 + e, G);
+    }
     const long long o = (long long)row * k_pad + k0;
     if (b.packed[j]) {
         *reinterpret_cast<f32x4*>(b.packed[j] + o) = f32x4{v[0], v[1], v[2], v[3]};
@@ -569,7 +603,8 @@ extern "C" int pu_pack_weights(const pu_pack_job* jobs, int n_jobs, void* stream
             b.mode[k] = J.mode; b.d0[k] = J.d0; b.d1[k] = J.d1; b.taps[k] = J.kh * J.kw;
             b.rows[k] = rows; b.k_pad[k] = J.k_pad; b.G[k] = J.cgroup;
             b.block_start[k] = blocks;
-            blocks += (int)(((long long)rows * (J.k_pad / 8) + 255) / 256);
+            const long long waves = (long long)((rows + 7) / 8) * ((J.k_pad / 8 + 7) / 8);
+            blocks += (int)((waves + 3) / 4);
             b.count++;
         }
         b.block_start[b.count] = blocks;
