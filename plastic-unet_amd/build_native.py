@@ -54,7 +54,8 @@ def _compile(src, force, defines=(), tag=""):
     deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(INCLUDE, "plastic_unet.h")]
     if not force and not _newer(deps, obj) and os.path.exists(obj + ".resources.txt"):
         return obj, None
-    cmd = [HIPCC] + CFLAGS + [RPASS] + ["-D" + d for d in defines] + ["-c", src, "-o", obj]
+    # an entry starting with '-' is passed as a raw compiler flag (ablation variants)
+    cmd = [HIPCC] + CFLAGS + [RPASS] + [d if d.startswith("-") else "-D" + d for d in defines] + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, "%s\n%s\n%s" % (" ".join(cmd), r.stdout, r.stderr)
