@@ -93,7 +93,9 @@ def source_hash(defines=()):
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
-    h.update(" ".join(CFLAGS + list(defines)).encode())
+    # flags with this checkout's absolute paths made relative: the id depends on content only
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    h.update(" ".join(CFLAGS + list(defines)).replace(root, "<root>").encode())
     return h.hexdigest()[:16]
 
 
