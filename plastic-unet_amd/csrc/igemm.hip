@@ -1071,7 +1071,7 @@ __global__ __launch_bounds__(256) void igemm_splitk_epilogue_kernel(const IgemmP
 // the float4 epilogue above applies bias / residual / ReLU / mask / split / accumulate.
 constexpr int SC_TH = 16, SC_TW = 32;
 
-template <int C, int N>
+template <int C, int N, int KP = (9 * C + 15) / 16 * 16>
 __global__ __launch_bounds__(256) void smallconv_kernel(const IgemmParams p) {
     constexpr int HH = SC_TH + 2, HWD = SC_TW + 2;
     constexpr int CP = (C + 3) & ~3;     // LDS channel stride (float4 reads when C % 4 == 0)
@@ -1119,37 +1119,28 @@ __global__ __launch_bounds__(256) void smallconv_kernel(const IgemmParams p) {
 
     const int row = threadIdx.x / (SC_TW / 2);
     const int col = (threadIdx.x % (SC_TW / 2)) * 2;
-    float acc0[N], acc1[N];
+    // accumulators packed over the thread's two pixels: one v_pk_fma_f32 per (channel, k) with the
+    // activation pair {x(col), x(col+1)} and the weight broadcast from a scalar register; the
+    // weight rows are KP floats apart (compile time), so the scalar loads take immediate offsets
+    // and need no scalar address arithmetic per step (the fmaf form spent ~50 SALU per step)
+    f32x2 acc[N];
 #pragma unroll
-    for (int n = 0; n < N; ++n) { acc0[n] = 0.f; acc1[n] = 0.f; }
-    // one (tap, 4-channel) step per iteration, not unrolled: only its 4*N weights are live
-    // (scalar registers, used directly as FMA operands)
+    for (int n = 0; n < N; ++n) acc[n] = f32x2{0.f, 0.f};
     constexpr int Q4 = CP / 4;
 #pragma unroll 1
     for (int step = 0; step < 9 * Q4; ++step) {
         const int tap = step / Q4, c4 = (step - tap * Q4) * 4;
         const int r = tap / 3, sx = tap - r * 3;
         const float* t0 = tile + ((row + r) * HWD + col + sx) * CP + c4;
-        const float* wt = p.wt + tap * C + c4;            // + n * k_pad: wave-uniform
-        // (packed v_pk_fma_f32 measured no faster: these layers are HBM-bound)
-        float a0[4], a1[4];
-        if (C % 4 == 0) {
-            const f32x4 v0 = *reinterpret_cast<const f32x4*>(t0);
-            const f32x4 v1 = *reinterpret_cast<const f32x4*>(t0 + CP);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { a0[e] = v0[e]; a1[e] = v1[e]; }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { a0[e] = t0[e]; a1[e] = t0[CP + e]; }
-        }
+        const float* wt = p.wt + (C % 4 == 0 ? 4 * step : step);   // tap * C + c4 (C % 4 == 0, or C == 1)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             if (e >= C) break;
+            const f32x2 a = {t0[e], t0[CP + e]};
 #pragma unroll
             for (int n = 0; n < N; ++n) {
-                const float w = wt[(long long)n * p.k_pad + e];
-                acc0[n] = fmaf(a0[e], w, acc0[n]);
-                acc1[n] = fmaf(a1[e], w, acc1[n]);
+                const float w = wt[n * KP + e];
+                acc[n] = __builtin_elementwise_fma(a, f32x2{w, w}, acc[n]);
             }
         }
     }
@@ -1164,7 +1155,7 @@ __global__ __launch_bounds__(256) void smallconv_kernel(const IgemmParams p) {
         for (int n = 0; n < N; n += 4) {
             f32x4 v;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = q ? acc1[n + e] : acc0[n + e];
+            for (int e = 0; e < 4; ++e) v[e] = acc[n + e][q];
             epi_store4(p, er, n, v);
         }
     }
@@ -1350,7 +1341,8 @@ static bool small_conv_ok(const pu_conv_args* a) {
     const bool nc = (a->n == 4) ? (C == 4 || C == 8 || C == 16) : true;
     return cset && nset && nc && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
            a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) && vec_epilogue(a) &&
-           (a->cgroup == 0 || a->cgroup >= C) && (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
+           (a->cgroup == 0 || a->cgroup >= C) && (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0)) &&
+           a->k_pad == (9 * C + 15) / 16 * 16;   // the kernel's compile-time weight row stride
 }
 
 // the single-channel stem: 3x3 / s1 / p1 (same size), C = 1, N in {32, 48, 64} (4-channel lane

@@ -29,6 +29,11 @@ LAYERS = {
     "l4_cat": (16, 512, 512, 256),
     "bottom": (8, 512, 0, 512),
     "stem": (128, 1, 0, 64),
+    # small-channel direct-kernel levels of C4/C5 (UNetpRes neurons 8 at 512^2, CoordConv base 8)
+    "s8": (512, 8, 0, 8),
+    "s8_cat": (512, 8, 8, 8),
+    "s16": (256, 16, 0, 16),
+    "s16_cat": (256, 16, 16, 16),
 }
 
 
@@ -82,10 +87,14 @@ def main():
                 r[k + "_TF"] = round(flops / (r[k + "_ms"] * 1e-3) / 1e12, 2)
                 r[k + "_frac"] = round(r[k + "_TF"] / peak, 3)
         r["gflop"] = flops / 1e9
+        px = B * H * H
+        r["fwd_GBs"] = round(4.0 * px * (c0 + c1 + cout) / (r.get("fwd_ms", 1e30) * 1e-3) / 1e9, 1)
+        r["dgrad_GBs"] = round(4.0 * px * (cout + 2 * (c0 + c1)) / (r.get("dgrad_ms", 1e30) * 1e-3) / 1e9, 1)
         res[name] = r
         print("%-8s H=%-3d %4d+%-4d->%-4d  fwd %7.3f ms %6.1f TF | dgrad %7.3f ms %6.1f TF | wgrad %7.3f ms %6.1f TF"
               % (name, H, c0, c1, cout, r.get("fwd_ms", 0), r.get("fwd_TF", 0), r.get("dgrad_ms", 0),
-                 r.get("dgrad_TF", 0), r.get("wgrad_ms", 0), r.get("wgrad_TF", 0)), flush=True)
+                 r.get("dgrad_TF", 0), r.get("wgrad_ms", 0), r.get("wgrad_TF", 0)) +
+              ("   [fwd %.0f GB/s, dgrad %.0f GB/s]" % (r["fwd_GBs"], r["dgrad_GBs"]) if c0 + c1 <= 16 else ""), flush=True)
     print("peak fp32 MFMA %.1f TF/s" % peak)
     if a.json:
         json.dump({"peak_TF": peak, "layers": res}, open(a.json, "w"), indent=1)
