@@ -41,6 +41,15 @@ expect_fail(lib.pu_bce_fwd(None, None, 0, None, None, 0, None))
 expect_fail(lib.pu_adam_multi(None, 1, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, None))
 bad = (L.AdamTensor * 3)(L.AdamTensor(A, A, A, A, 10), L.AdamTensor(A, None, A, A, 10), L.AdamTensor())
 expect_fail(lib.pu_adam_multi(bad, 3, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1.0, None))
+expect_fail(lib.pu_pack_weights(None, 1, None))
+jobs = (L.PackJob * 3)(L.PackJob(A, A, None, A, 0, 64, 64, 3, 3, 576, 32),    # valid
+                       L.PackJob(A, A, None, None, 7, 64, 64, 3, 3, 576, 0),    # bad mode
+                       L.PackJob(A, None, None, None, 0, 64, 64, 3, 3, 576, 0)) # no output
+expect_fail(lib.pu_pack_weights(jobs, 3, None))
+jobs = (L.PackJob * 1)(L.PackJob(A, A + 4, None, None, 0, 64, 64, 3, 3, 576, 0))   # misaligned output
+expect_fail(lib.pu_pack_weights(jobs, 1, None))
+jobs = (L.PackJob * 1)(L.PackJob(A, A, None, A, 0, 64, 64, 3, 3, 568, 0))       # k_pad < 9 * 64
+expect_fail(lib.pu_pack_weights(jobs, 1, None))
 h = L.PlasticHeadArgs(2, 100, 64, A, 0, A, A, A, A, A, A, A, A, A, 1)          # nbf not a multiple of 16
 expect_fail(lib.pu_plastic_head_fwd(ctypes.byref(h), None))
 h = L.PlasticHeadArgs(2, 128, 64, A, 0, A, A, A, A, A, A, A, A, A, 1)          # hebb_out aliasing hebb
