@@ -553,14 +553,21 @@ __device__ __forceinline__ int hx_off(int row, int col) {   // byte offset in a 
     return row * 128 + 16 * ((col >> 3) ^ (((row >> 1) & 1) << 2)) + 2 * (col & 7);
 }
 
-__global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p) {
-    constexpr int XG = 4;                     // X float4 groups per thread (864 = 3 x 256 + 96)
-    __shared__ __attribute__((aligned(16))) char lds[2 * 3 * HX_IMG];
+// NT = 64-channel output tiles per block: NT = 1 is 4 waves (two blocks per CU); NT = 2 is 8 waves
+// (one block per CU) sharing each loaded and split X halo between 128 output channels - half the
+// X reads and splits per MFMA, 12 instead of 20 raw-row registers per thread.
+template <int NT>
+__global__ __launch_bounds__(256 * NT) void wgrad_halo_x6_kernel(const WgradParams p) {
+    constexpr int NTH = 256 * NT;
+    constexpr int RS = NTH / 16;              // halo rows per X group (16 NT: keeps the row swizzle)
+    constexpr int XG = (HX_ROWS + RS - 1) / RS;   // X float4 groups per thread (864 = 3 x 256 + 96 | 512 + 352)
+    constexpr int IMG = (HX_ROWS + 16 * NT) * 128;  // one plane: 54 X rows, then NT x 16 dZ rows
+    __shared__ __attribute__((aligned(16))) char lds[2 * 3 * IMG];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ci = wave & 1, nj = wave >> 1;
+    const int ci = wave & 1, nj = (wave >> 1) & 1, nt = wave >> 2;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int tx = tile % p.gx;               // 64-channel input tile
     const int tyz = tile / p.gx;
@@ -570,7 +577,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     const int m_end = min(p.M, m_begin + p.mps);
     const int T = m_end > m_begin ? (m_end - m_begin) / 16 : 0;
 
-    // ---- thread roles in the loads: column quad cq (fixed), halo pixel rows hp_i = tid/16 + 16 i
+    // ---- thread roles in the loads: column quad cq (fixed), halo pixel rows hp_i = tid/16 + RS i
     const int cq = tid & 15;
     const int c_lo = tx * 64;                 // first input channel of the tile
     const bool first = c_lo < p.c0;
@@ -580,14 +587,16 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     unsigned x_cls[XG];                       // edge classes: 1 top, 2 bottom, 4 left, 8 right, 16 past the halo, 32 all
 #pragma unroll
     for (int i = 0; i < XG; ++i) {
-        const int hp = (tid >> 4) + 16 * i;
+        const int hp = (tid >> 4) + RS * i;
         const int rr = hp / 18, cc = hp - rr * 18;
         x_lane[i] = xsrc + (long long)((rr - 1) * p.Wi + (cc - 1)) * cs + cq * 4;
         if (hp >= HX_ROWS) x_lane[i] = g_wg_zero16;   // rows past the halo: class 16 -> zero page, never stored
         x_cls[i] = 32u | (hp >= HX_ROWS ? 16u
                                         : ((rr == 0 ? 1u : 0u) | (rr == 2 ? 2u : 0u) | (cc == 0 ? 4u : 0u) | (cc == 17 ? 8u : 0u)));
     }
-    const float* p_lane = p.P + (long long)(tid >> 4) * p.N + ty * 64 + cq * 4;
+    // dZ roles: row prow of the stage, channel quad pq of the block's 64 NT output channels
+    const int pq = tid % (16 * NT), prow = tid / (16 * NT);
+    const float* p_lane = p.P + (long long)prow * p.N + ty * 64 * NT + pq * 4;
 
     f32x4 rx[XG], rp;
     auto load = [&](int t) {                  // raw rows of stage t into registers (branch-free:
@@ -612,12 +621,12 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     };
     f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
     const bool bias_blk = p.bias_mode == 1 && tx == 0;
-    // plane writes: halo rows hp_i = hp_0 + 16 i keep the swizzle of hp_0 (16 i = 0 mod 4), so
+    // plane writes: halo rows hp_i = hp_0 + RS i keep the swizzle of hp_0 (RS i = 0 mod 4), so
     // every write of a thread is one base address plus an immediate
     const int w_base = hx_off(tid >> 4, cq * 4);
-    const int wp_base = hx_off(HX_ROWS + (tid >> 4), cq * 4);
+    const int wp_base = hx_off(HX_ROWS + 16 * (pq >> 4) + prow, (pq & 15) * 4);
     auto split_store = [&](int buf) {         // registers -> bf16 planes of buffer buf
-        char* pb = lds + buf * 3 * HX_IMG;
+        char* pb = lds + buf * 3 * IMG;
         auto put = [&](char* dst, const f32x4 v) {
             unsigned h[2], m[2], l[2];
 #pragma unroll
@@ -636,13 +645,13 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
             }
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
             *reinterpret_cast<u32x2*>(dst) = u32x2{h[0], h[1]};
-            *reinterpret_cast<u32x2*>(dst + HX_IMG) = u32x2{m[0], m[1]};
-            *reinterpret_cast<u32x2*>(dst + 2 * HX_IMG) = u32x2{l[0], l[1]};
+            *reinterpret_cast<u32x2*>(dst + IMG) = u32x2{m[0], m[1]};
+            *reinterpret_cast<u32x2*>(dst + 2 * IMG) = u32x2{l[0], l[1]};
         };
 #pragma unroll
         for (int i = 0; i < XG; ++i) {
-            const int hp = (tid >> 4) + 16 * i;
-            if (i < 3 || hp < HX_ROWS) put(pb + w_base + i * 16 * 128, rx[i]);
+            const int hp = (tid >> 4) + RS * i;
+            if (i < XG - 1 || hp < HX_ROWS) put(pb + w_base + i * RS * 128, rx[i]);
         }
         put(pb + wp_base, rp);
         if (bias_blk) bsum += rp;
@@ -664,7 +673,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     int xb[4];
 #pragma unroll
     for (int res = 0; res < 4; ++res) xb[res] = hx_off(res + rsub, ci * 32 + ccol);
-    const int pbase = hx_off(HX_ROWS + rsub, nj * 32 + ccol);
+    const int pbase = hx_off(HX_ROWS + 16 * nt + rsub, nj * 32 + ccol);
     auto tr2 = [&](const char* a) {           // rows +0 / +4 of a fragment -> one MFMA operand
         const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a);
         const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a + 4 * 128));
@@ -674,13 +683,13 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
     };
     auto mfma_stage = [&](auto bufc) {
         constexpr int buf = decltype(bufc)::value;
-        const char* pb = lds + buf * 3 * HX_IMG;
-        const wg_bf16x8 ph = tr2(pb + pbase), pm = tr2(pb + HX_IMG + pbase), pl = tr2(pb + 2 * HX_IMG + pbase);
+        const char* pb = lds + buf * 3 * IMG;
+        const wg_bf16x8 ph = tr2(pb + pbase), pm = tr2(pb + IMG + pbase), pl = tr2(pb + 2 * IMG + pbase);
 #pragma unroll
         for (int t9 = 0; t9 < 9; ++t9) {
             const int row0 = (t9 / 3) * 18 + (t9 % 3);
             const char* xa = pb + xb[row0 & 3] + (row0 & ~3) * 128;
-            const wg_bf16x8 qh = tr2(xa), qm = tr2(xa + HX_IMG), ql = tr2(xa + 2 * HX_IMG);
+            const wg_bf16x8 qh = tr2(xa), qm = tr2(xa + IMG), ql = tr2(xa + 2 * IMG);
             f32x16 c = acc[t9];
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm, c, 0, 0, 0);   // small terms first
             c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph, c, 0, 0, 0);
@@ -723,15 +732,15 @@ __global__ __launch_bounds__(256) void wgrad_halo_x6_kernel(const WgradParams p)
         f32x4* red = reinterpret_cast<f32x4*>(lds);
         red[tid] = bsum;
         __syncthreads();
-        if (tid < 16) {
+        if (tid < 16 * NT) {
             f32x4 v = red[tid];
-            for (int r = 1; r < 16; ++r) v += red[r * 16 + tid];
+            for (int r = 1; r < 16; ++r) v += red[r * 16 * NT + tid];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) slab[(long long)(ty * 64 + tid * 4 + e) * p.Kcp + p.K] = v[e];
+            for (int e = 0; e < 4; ++e) slab[(long long)(ty * 64 * NT + tid * 4 + e) * p.Kcp + p.K] = v[e];
         }
     }
     const int lr = lane & 31, lh = lane >> 5;
-    const int n = ty * 64 + nj * 32 + lr;
+    const int n = ty * 64 * NT + nt * 64 + nj * 32 + lr;
 #pragma unroll
     for (int t9 = 0; t9 < 9; ++t9) {
 #pragma unroll
@@ -1012,6 +1021,7 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
 struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
     bool qvec, dma, small, halo, stem;
+    int nt = 1;                               // halo kernel: 64-channel output tiles per block
     int tiles_w, tiles_h;
     size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
     size_t part_bytes() const { return G > 1 ? (size_t)G * Nr * Kcp * sizeof(double) : 0; }
@@ -1099,17 +1109,18 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
         a->in_h == a->out_h && a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 &&
         a->n % 64 == 0 && a->bias_mode != 2 && (long long)a->batch * a->in_h * a->in_w * (pl->C) < (1LL << 31)) {
         pl->halo = true;
-        pl->BN = 64;
+        pl->nt = a->n % 128 == 0 ? 2 : 1;    // 128 output channels per block when they divide
+        pl->BN = 64 * pl->nt;
         pl->BK = 9 * 64;
-        const int tiles = (pl->C / 64) * (a->n / 64);
-        int splits = 512 / tiles;                     // two 4-wave blocks per CU
+        const int tiles = (pl->C / 64) * (a->n / pl->BN);
+        int splits = (pl->nt == 2 ? 256 : 512) / tiles;   // one 8-wave / two 4-wave blocks per CU
         const int stages = (int)(M / 16);
         if (splits > stages) splits = stages;
         if (splits < 1) splits = 1;
         pl->mps = ceil_div(stages, splits) * 16;
         pl->splits = ceil_div((int)M, pl->mps);
         pl->gx = pl->C / 64;
-        pl->gy = a->n / 64;
+        pl->gy = a->n / pl->BN;
         const long long total = (long long)pl->Nr * pl->Kcp;
         int G = (int)ceil_div(262144LL, total);
         const int by_len = ceil_div(pl->splits, 8);
@@ -1689,7 +1700,8 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
     } while (0)
 #define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
         if (pl.halo) {
-            hipLaunchKernelGGL(wgrad_halo_x6_kernel, grid, dim3(256), 0, s, p);
+            if (pl.nt == 2) hipLaunchKernelGGL(wgrad_halo_x6_kernel<2>, grid, dim3(512), 0, s, p);
+            else hipLaunchKernelGGL(wgrad_halo_x6_kernel<1>, grid, dim3(256), 0, s, p);
         } else if (pl.dma) {
             if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
             else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);

@@ -20,6 +20,8 @@ import sys
 
 
 def tag_of(name):
+    if "wgrad_halo_x6_kernel<2>" in name:
+        return "wgrad<128x576,halo,x6>"
     if "wgrad_halo_x6_kernel" in name:
         return "wgrad<64x576,halo,x6>"
     m = re.search(r"igemm_x6_lean_kernel<(\d+), (\d+),", name)
