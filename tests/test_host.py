@@ -114,3 +114,20 @@ def test_batch_prefetcher_order_shards_and_slot_rotation():
                     seen.append((lo, hi))
                 assert seen == ranges
     assert list(BatchPrefetcher(X, Y, [], "cpu")) == []
+
+
+def test_pmc_kernel_tags_match_bench_tags():
+    """tools/pmc_traffic.py keys the PMC bytes by the same kernel tags bench.py's KernelProfiler
+    uses (kernels.py), so roofline.traffic finds the dominant kernel's entry."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("pmc_traffic", os.path.join(root, "tools", "pmc_traffic.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    assert m.tag_of("void pu::wgrad_halo_x6_kernel<2>(pu::WgradParams)") == "wgrad<128x576,halo,x6>"
+    assert m.tag_of("void pu::wgrad_halo_x6_kernel<1>(pu::WgradParams)") == "wgrad<64x576,halo,x6>"
+    assert m.tag_of("void pu::igemm_x6_lean_kernel<256, 64, 4, 1, 4, 2>(pu::IgemmParams)") == "igemm<256x64,x6>"
+    assert m.tag_of("void pu::wgrad_dma_kernel<128, 256, 2, 2, 3, true, 4, true>(pu::WgradParams)") == \
+        "wgrad<128x256,vec4,x6>"
+    assert m.tag_of("pu::adam_kernel(pu::AdamBatch, float, float, float, float, float, float, float)") == "adam"
