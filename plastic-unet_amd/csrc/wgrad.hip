@@ -1372,18 +1372,20 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(const WgradBf16Params p
 // transposed reads, same 4-wave (channel half, output half) x 9-tap accumulator layout, same
 // slab partials.  Two stages (32 output pixels) per barrier: the bf16 MFMA work of one stage
 // (9 x 32 cycles per wave) is too short to hide a barrier.  Requirements as the x6 kernel.
-constexpr int HB_IMG = (HX_ROWS + 16) * 128;  // bytes of one stage's plane (X rows, then 16 dZ rows)
 
-__global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Params p) {
-    constexpr int XG = 4;                     // halo row groups per thread (54 rows = 3 x 16 + 6)
+template <int NT>                             // 64-channel output tiles per block (as the x6 kernel)
+__global__ __launch_bounds__(256 * NT) void wgrad_halo_bf16_kernel(const WgradBf16Params p) {
+    constexpr int RS = 16 * NT;               // halo rows per row group
+    constexpr int XG = (HX_ROWS + RS - 1) / RS;   // halo row groups per thread (54 = 3 x 16 + 6 | 32 + 22)
     constexpr int SPB = 2;                    // stages per barrier
-    __shared__ __attribute__((aligned(16))) char lds[2 * SPB * HB_IMG];
+    constexpr int IMG = (HX_ROWS + 16 * NT) * 128;  // one stage's plane: 54 X rows, then NT x 16 dZ rows
+    __shared__ __attribute__((aligned(16))) char lds[2 * SPB * IMG];
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ci = wave & 1, nj = wave >> 1;
+    const int ci = wave & 1, nj = (wave >> 1) & 1, nt = wave >> 2;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int tx = tile % p.gx;               // 64-channel input tile
     const int tyz = tile / p.gx;
@@ -1403,14 +1405,15 @@ __global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Par
     unsigned x_cls[XG];                       // edge classes: 1 top, 2 bottom, 4 left, 8 right, 16 past the halo, 32 all
 #pragma unroll
     for (int i = 0; i < XG; ++i) {
-        const int hp = (tid >> 4) + 16 * i;
+        const int hp = (tid >> 4) + RS * i;
         const int rr = hp / 18, cc = hp - rr * 18;
         x_lane[i] = xsrc + (long long)((rr - 1) * p.Wi + (cc - 1)) * cs + cq * 4;
         if (hp >= HX_ROWS) x_lane[i] = zero;
         x_cls[i] = 32u | (hp >= HX_ROWS ? 16u
                                         : ((rr == 0 ? 1u : 0u) | (rr == 2 ? 2u : 0u) | (cc == 0 ? 4u : 0u) | (cc == 17 ? 8u : 0u)));
     }
-    const __bf16* p_lane = p.P + (long long)(tid >> 4) * p.N + ty * 64 + cq * 4;
+    const int pq = tid % (16 * NT), prow = tid / (16 * NT);   // dZ row and channel quad
+    const __bf16* p_lane = p.P + (long long)prow * p.N + ty * 64 * NT + pq * 4;
 
     u32x2 rx[SPB][XG], rp[SPB];
     auto load = [&](int t, int j) {           // raw bf16 rows of stage t into register set j
@@ -1435,13 +1438,13 @@ __global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Par
     f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
     const bool bias_blk = p.bias_mode == 1 && tx == 0;
     const int w_base = hx_off(tid >> 4, cq * 4);
-    const int wp_base = hx_off(HX_ROWS + (tid >> 4), cq * 4);
+    const int wp_base = hx_off(HX_ROWS + 16 * (pq >> 4) + prow, (pq & 15) * 4);
     auto store = [&](int buf, int j, bool live) {   // register set j -> plane j of buffer buf
-        char* pb = lds + (buf * SPB + j) * HB_IMG;
+        char* pb = lds + (buf * SPB + j) * IMG;
 #pragma unroll
         for (int i = 0; i < XG; ++i) {
-            const int hp = (tid >> 4) + 16 * i;
-            if (i < 3 || hp < HX_ROWS) *reinterpret_cast<u32x2*>(pb + w_base + i * 16 * 128) = rx[j][i];
+            const int hp = (tid >> 4) + RS * i;
+            if (i < XG - 1 || hp < HX_ROWS) *reinterpret_cast<u32x2*>(pb + w_base + i * RS * 128) = rx[j][i];
         }
         *reinterpret_cast<u32x2*>(pb + wp_base) = rp[j];
         if (bias_blk && live) {
@@ -1464,7 +1467,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Par
     int xb[4];
 #pragma unroll
     for (int res = 0; res < 4; ++res) xb[res] = hx_off(res + rsub, ci * 32 + ccol);
-    const int pbase = hx_off(HX_ROWS + rsub, nj * 32 + ccol);
+    const int pbase = hx_off(HX_ROWS + 16 * nt + rsub, nj * 32 + ccol);
     auto tr2 = [&](const char* a) {
         const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a);
         const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a + 4 * 128));
@@ -1487,7 +1490,7 @@ __global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Par
     auto group = [&](int g, auto bufc) {
         constexpr int buf = decltype(bufc)::value;
 #pragma unroll
-        for (int j = 0; j < SPB; ++j) mfma_plane(lds + (buf * SPB + j) * HB_IMG);
+        for (int j = 0; j < SPB; ++j) mfma_plane(lds + (buf * SPB + j) * IMG);
         if (g + 1 < NG) {
 #pragma unroll
             for (int j = 0; j < SPB; ++j) store(buf ^ 1, j, SPB * (g + 1) + j < T);
@@ -1522,15 +1525,15 @@ __global__ __launch_bounds__(256) void wgrad_halo_bf16_kernel(const WgradBf16Par
         f32x4* red = reinterpret_cast<f32x4*>(lds);
         red[tid] = bsum;
         __syncthreads();
-        if (tid < 16) {
+        if (tid < 16 * NT) {
             f32x4 v = red[tid];
-            for (int r = 1; r < 16; ++r) v += red[r * 16 + tid];
+            for (int r = 1; r < 16; ++r) v += red[r * 16 * NT + tid];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) slab[(long long)(ty * 64 + tid * 4 + e) * p.Kcp + p.K] = v[e];
+            for (int e = 0; e < 4; ++e) slab[(long long)(ty * 64 * NT + tid * 4 + e) * p.Kcp + p.K] = v[e];
         }
     }
     const int lr = lane & 31, lh = lane >> 5;
-    const int n = ty * 64 + nj * 32 + lr;
+    const int n = ty * 64 * NT + nt * 64 + nj * 32 + lr;
 #pragma unroll
     for (int t9 = 0; t9 < 9; ++t9) {
 #pragma unroll
@@ -1596,12 +1599,13 @@ static int plan_wgrad_bf16(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->halo = a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->out_h &&
                a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 && a->n % 64 == 0 &&
                a->bias_mode != 2 && M * pl->C < (1LL << 31);
-    if (pl->halo) {                   // wgrad_halo_bf16_kernel: 64 x 64 x 9-tap tiles, two blocks per CU
-        pl->BN = 64; pl->BK = 9 * 64;
+    if (pl->halo) {                   // wgrad_halo_bf16_kernel: 64 NT x 64 x 9-tap tiles, 512 NT-thread blocks
+        pl->nt = a->n % 128 == 0 ? 2 : 1;
+        pl->BN = 64 * pl->nt; pl->BK = 9 * 64;
         pl->gx = pl->C / 64;
-        pl->gy = a->n / 64;
+        pl->gy = a->n / pl->BN;
         const int stages = (int)(M / 16);
-        int splits = 512 / (pl->gx * pl->gy);
+        int splits = (pl->nt == 2 ? 256 : 512) / (pl->gx * pl->gy);   // one 8-wave / two 4-wave blocks per CU
         if (splits > stages) splits = stages;
         if (splits < 1) splits = 1;
         pl->mps = ceil_div(stages, splits) * 16;
@@ -1752,7 +1756,8 @@ extern "C" int pu_wgrad_bf16_phase(const pu_wgrad_args* a, void* workspace, size
         p.slab = (float*)workspace; p.mps = pl.mps; p.gx = pl.gx; p.gy = pl.gy;
         p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
         p.dC = make_fastdiv(pl.C); p.dKw = make_fastdiv(a->kw);
-        if (pl.halo) hipLaunchKernelGGL(wgrad_halo_bf16_kernel, dim3(pl.gx * pl.gy * pl.splits), dim3(256), 0, s, p);
+        if (pl.halo && pl.nt == 2) hipLaunchKernelGGL(wgrad_halo_bf16_kernel<2>, dim3(pl.gx * pl.gy * pl.splits), dim3(512), 0, s, p);
+        else if (pl.halo) hipLaunchKernelGGL(wgrad_halo_bf16_kernel<1>, dim3(pl.gx * pl.gy * pl.splits), dim3(256), 0, s, p);
         else hipLaunchKernelGGL(wgrad_bf16_kernel, dim3(pl.gx * pl.gy * pl.splits), dim3(256), 0, s, p);
         st = check_launch("pu_wgrad_bf16 (gemm)");
         if (st != PU_OK) return st;
