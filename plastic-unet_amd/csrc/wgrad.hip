@@ -1018,6 +1018,46 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
     }
 }
 
+// pass 2 with coalesced stores: block (c chunk of 64, row n) sums slab[.][n][tap*C + c] for its
+// 64 channels x taps (thread = (tap, c): 256-B coalesced reads per tap), transposes through LDS
+// and stores the contiguous [c][kh][kw] run of dweight[n] (the scatter above writes 4 B at a
+// 4*taps-byte stride).  Same fixed-order fp64 chains as wgrad_finish_kernel, so bit-identical.
+// bias_mode 0/1 (the ConvT bias, mode 2, stays on wgrad_finish_kernel).
+template <typename T>
+__global__ __launch_bounds__(576) void wgrad_finish_t_kernel(const T* __restrict__ part, int G, int Nr, int Kc, int K,
+                                                              int C, int taps, int bias_mode, float* __restrict__ dw,
+                                                              float* __restrict__ db, int accumulate) {
+    __shared__ float tr[576];
+    const long long total = (long long)Nr * Kc;
+    const int n = blockIdx.y;
+    const int c0 = blockIdx.x * 64;
+    const int tap = threadIdx.x >> 6, c = c0 + (threadIdx.x & 63);
+    auto sum = [&](long long idx) {
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int g = 0;
+        for (; g + 3 < G; g += 4) {
+            s0 += (double)part[(long long)g * total + idx];
+            s1 += (double)part[(long long)(g + 1) * total + idx];
+            s2 += (double)part[(long long)(g + 2) * total + idx];
+            s3 += (double)part[(long long)(g + 3) * total + idx];
+        }
+        for (; g < G; ++g) s0 += (double)part[(long long)g * total + idx];
+        return (float)((s0 + s1) + (s2 + s3));
+    };
+    if (c < C) tr[(c - c0) * taps + tap] = sum((long long)n * Kc + tap * C + c);
+    if (bias_mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+        const float v = sum((long long)n * Kc + K);
+        db[n] = accumulate ? db[n] + v : v;
+    }
+    __syncthreads();
+    const int cn = min(64, C - c0);
+    if ((int)threadIdx.x < cn * taps) {
+        float* o = dw + ((long long)n * C + c0) * taps + threadIdx.x;
+        const float v = tr[threadIdx.x];
+        *o = accumulate ? *o + v : v;
+    }
+}
+
 struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
     bool qvec, dma, small, halo, stem;
@@ -1553,6 +1593,22 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
     const long long total = (long long)pl.Nr * pl.Kcp;
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
     const dim3 fgrid((unsigned)((threads + 255) / 256));
+    const int taps = a->kh * a->kw;
+    if (a->bias_mode != 2 && taps <= 9) {
+        const dim3 tgrid((unsigned)ceil_div(pl.C, 64), (unsigned)a->n);
+        const dim3 tblock((unsigned)(64 * taps));
+        if (pl.G == 1) {
+            hipLaunchKernelGGL(wgrad_finish_t_kernel<float>, tgrid, tblock, 0, s, (const float*)workspace, pl.splits,
+                               pl.Nr, pl.Kcp, pl.K, pl.C, taps, a->bias_mode, a->dweight, a->dbias, a->accumulate);
+        } else {
+            double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
+            hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
+                               (const float*)workspace, pl.splits, total, pl.G, part);
+            hipLaunchKernelGGL(wgrad_finish_t_kernel<double>, tgrid, tblock, 0, s, (const double*)part, pl.G, pl.Nr,
+                               pl.Kcp, pl.K, pl.C, taps, a->bias_mode, a->dweight, a->dbias, a->accumulate);
+        }
+        return check_launch("pu_wgrad (reduce)");
+    }
     if (pl.G == 1) {
         hipLaunchKernelGGL(wgrad_finish_kernel<float>, fgrid, dim3(256), 0, s, (const float*)workspace, pl.splits,
                            pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,

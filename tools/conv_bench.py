@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--layers", default=",".join(LAYERS))
     ap.add_argument("--json", default=None)
     ap.add_argument("--ops", default="fwd,dgrad,wgrad", help="subset of fwd,dgrad,wgrad to time")
+    ap.add_argument("--data", default="randn", choices=["randn", "bf16", "zeros"],
+                    help="operand values (power/clock probe): bf16 = values exact in bf16 (zero mid/lo planes)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     cu, clk, _ = K.device_info(0)
@@ -71,6 +73,10 @@ def main():
         w = torch.randn(cout, c0 + c1, 3, 3, device=dev, generator=g) * 0.05
         b = torch.randn(cout, device=dev, generator=g)
         dz = torch.randn(B, H, H, cout, device=dev, generator=g)
+        if a.data != "randn":
+            for t in (x0, x1, w, dz):
+                if t is not None:
+                    t.copy_(t.bfloat16().float() if a.data == "bf16" else torch.zeros_like(t))
         pk = T._Packs()
         flops = 2.0 * B * H * H * cout * 9 * (c0 + c1)
         r = {}
