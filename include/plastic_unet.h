@@ -92,10 +92,7 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
  *   over ksplit blocks per tile; the partial tiles go to the workspace and a second kernel sums
  *   them in fixed split order (deterministic) and runs the epilogue above.  NULL -> no split.
  * ------------------------------------------------------------------------------------------- */
-/* PU_CONV_NO_HALO: a dispatch hint, not an epilogue flag - keep a 3x3/s1 layer that the halo
- * kernel would take (x6 operands, width 32/64/128) on the per-tap implicit-GEMM kernel (A/B and
- * parity tests; both compute the same sums, bit-identical with cgroup 16) */
-enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8, PU_CONV_NO_HALO = 16 };
+enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8 };
 
 typedef struct {
     int batch;

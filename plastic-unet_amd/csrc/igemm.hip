@@ -1025,221 +1025,6 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_lean_kernel(const IgemmParam
     }
 }
 
-// ---------------------------------------------------------------- halo 6-product kernel
-// 3x3 / stride 1 / pad 1 convolutions (fwd and dgrad) whose image width W is 32, 64 or 128:
-// the lean kernel loads and splits every input element once per tap (9 times), this one once.
-// A block owns R whole output rows of one image (R * W = 512 pixels) x 64 output channels; per
-// 16-channel K chunk it loads the (R+2) x (W+2) input halo once (fp32, global -> registers one
-// chunk ahead), splits each element once into hi/mid/lo bf16 and stores them to LDS as
-// [pixel][plane][16 channels] with a 112-B pixel stride (7 bank quads: any 16 consecutive pixels
-// hit distinct quads, so ds_read_b128 fragment reads are conflict-free at every tap shift and
-// every fragment address is one base register + an immediate), and copies the chunk's pre-split
-// weight planes of all 9 taps ([tap][plane][n][32 B], halves swizzled by n bit 3).  Tap (r, s) of
-// a 32-pixel fragment is the halo window at row r, column s: 9 taps x 2 x 2 fragments x 6 MFMAs
-// per wave per chunk from one LDS image, two barriers per chunk.  8 waves, each 64 pixels x 64
-// channels.  K order and MFMA order per accumulator are the lean kernel's, so with cgroup 16 the
-// two are bit-identical.  Requirements (host: halo_ok).
-constexpr int HC_NT = 512;              // threads per block
-constexpr int HC_BN = 64;               // output channels per block
-constexpr int HC_PX = 112;              // LDS bytes per halo pixel (3 planes x 32 B + 16 pad)
-
-template <int W>
-__global__ __launch_bounds__(HC_NT) void igemm_halo_x6_kernel(const IgemmParams p) {
-    constexpr int R = 512 / W;
-    constexpr int HW = W + 2;
-    constexpr int HP = (R + 2) * HW;                  // halo pixels
-    constexpr int XB = HP * HC_PX;
-    constexpr int WB = 9 * 3 * HC_BN * 32;            // weight planes [tap][plane][n][32 B]
-    constexpr int ITEMS = 2 * HP;                     // (8-channel half, halo pixel) items
-    constexpr int IT = (ITEMS + HC_NT - 1) / HC_NT;
-    constexpr int WPC = 9 * 6 * HC_BN;                // 16-B weight pieces per chunk
-    constexpr int WIT = (WPC + HC_NT - 1) / HC_NT;
-    constexpr unsigned NONE = 0xffffffffu;
-    static_assert(R * W == 512 && W % 32 == 0, "halo tile");
-
-    __shared__ __attribute__((aligned(16))) char lds[XB + WB];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lr = lane & 31, lh = lane >> 5;
-
-    // persistent blocks: XCD x = blockIdx % 8 owns the contiguous tile range [x*tq, (x+1)*tq) (the
-    // output tiles of one row block, which share its halo, and neighbouring row blocks stay on one
-    // L2); its blocks stride through it.  Tile = row block * gn + output-channel tile.
-    const int ntiles = p.M / 512 * p.gn;
-    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
-    const int tq = (ntiles + 7) >> 3;
-    const int t_end = min(ntiles, (xcd + 1) * tq);
-    int tile = xcd * tq + (int)(blockIdx.x >> 3);
-    if (tile >= t_end) return;                        // uniform per block
-    const int rb = p.Ho / R;                          // row blocks per image
-
-    // halo items of this thread (half-major: 8 consecutive lanes store 8 consecutive pixels):
-    // source element offset of the pixel's 8 channels (-1: zero padding), LDS offset
-    int xsrc[IT];
-    unsigned xoff[IT];
-    int xhalf[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-        const int e = it * HC_NT + tid;
-        const int half = e >= HP, hp = e - half * HP;
-        xoff[it] = e < ITEMS ? (unsigned)(hp * HC_PX + half * 16) : NONE;
-        xhalf[it] = half * 8;
-    }
-    auto setup = [&](int t) {                         // source pixels of tile t's halo
-        const int mt = t / p.gn;
-        const int b = mt / rb;
-        const int r0 = (mt - b * rb) * R;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int e = it * HC_NT + tid;
-            const int hp = e - (e >= HP ? HP : 0);
-            const int hr = hp / HW, hc = hp - hr * HW;
-            const int ir = r0 - 1 + hr, ic = hc - 1;
-            const bool ok = e < ITEMS && (unsigned)ir < (unsigned)p.Hi && (unsigned)ic < (unsigned)W;
-            xsrc[it] = ok ? ((b * p.Hi + ir) * W + ic) : -1;
-        }
-    };
-    // weight pieces (tap, plane, n, half): global offset within the chunk's stages (without the
-    // tile's first channel), LDS offset
-    const int cg = p.cgroup / 16;                     // 1 or 2 (16- or 32-channel K groups)
-    unsigned wgo[WIT], wlo[WIT];
-#pragma unroll
-    for (int w = 0; w < WIT; ++w) {
-        const int e = w * HC_NT + tid;
-        const int half = e & 1, n = (e >> 1) & 63, tp = e >> 7;   // tp = tap * 3 + plane
-        const int tap = tp / 3, pl = tp - 3 * tap;
-        wgo[w] = (unsigned)(((tap * cg * 6 + pl * 2 + half) * p.N + n) * 16);
-        wlo[w] = e < WPC ? (unsigned)(XB + (tp * HC_BN + n) * 32 + ((half ^ ((n >> 3) & 1)) << 4)) : NONE;
-    }
-    const unsigned stage_bytes = (unsigned)p.N * 96u;   // one 16-k stage's six planes
-
-    f32x4 xr[IT][2];
-    f32x4 wr[WIT];
-    auto load = [&](int j, int n_blk) {
-        const int c = j * 16;
-        const bool second = c >= p.c0;
-        const float* src = second ? p.src1 : p.src0;
-        const int cs = second ? p.c1 : p.c0;
-        const int cc = second ? c - p.c0 : c;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            xr[it][0] = xr[it][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (xsrc[it] >= 0) {
-                const float* sp = src + xsrc[it] * cs + cc + xhalf[it];
-                xr[it][0] = *reinterpret_cast<const f32x4*>(sp);
-                xr[it][1] = *reinterpret_cast<const f32x4*>(sp + 4);
-            }
-        }
-        const unsigned sbase = (unsigned)((j / cg) * 9 * cg + (j % cg)) * stage_bytes + (unsigned)n_blk * 16u;
-        const char* wsrc = reinterpret_cast<const char*>(p.wt) + sbase;
-#pragma unroll
-        for (int w = 0; w < WIT; ++w)
-            if (wlo[w] != NONE) wr[w] = *reinterpret_cast<const f32x4*>(wsrc + wgo[w]);
-    };
-    auto store = [&]() {
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            if (xoff[it] != NONE) {
-                bf16x8_t h, m, l;
-                split3_pairs(xr[it][0], xr[it][1], h, m, l);
-                *reinterpret_cast<bf16x8_t*>(lds + xoff[it]) = h;
-                *reinterpret_cast<bf16x8_t*>(lds + xoff[it] + 32) = m;
-                *reinterpret_cast<bf16x8_t*>(lds + xoff[it] + 64) = l;
-            }
-        }
-#pragma unroll
-        for (int w = 0; w < WIT; ++w)
-            if (wlo[w] != NONE) *reinterpret_cast<f32x4*>(lds + wlo[w]) = wr[w];
-    };
-
-    // fragment i of this wave = output pixels p0 + 32 i .. + 31 of the block (one image row);
-    // its tap (r, s) window starts at halo pixel (row + r) * HW + col + s
-    const int p0 = wave * 64;
-    const int orow = p0 / W, ocol = p0 - orow * W;
-    const unsigned xa = (unsigned)(((orow * HW + ocol) + lr) * HC_PX + lh * 16);
-    constexpr int FRAG1 = (32 / W) * HW + (32 % W);     // halo pixels from fragment 0 to 1
-    const unsigned wa = (unsigned)(XB + lr * 32 + ((lh ^ ((lr >> 3) & 1)) << 4));
-    auto rd_w = [&](int t, int jj, bf16x8_t (&f)[3]) {
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-            f[pl] = *reinterpret_cast<const bf16x8_t*>(lds + wa + ((t * 3 + pl) * HC_BN + jj * 32) * 32);
-    };
-    auto rd_x = [&](int t, int i, bf16x8_t (&f)[3]) {
-        const int toff = ((t / 3) * HW + (t % 3) + i * FRAG1) * HC_PX;
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) f[pl] = *reinterpret_cast<const bf16x8_t*>(lds + xa + toff + pl * 32);
-    };
-    // the lean kernel's product order (smallest terms first), planes 0/1/2 = hi/mid/lo
-    auto mm6 = [&](const bf16x8_t (&w)[3], const bf16x8_t (&x)[3], f32x16& acc) {
-        f32x16 c = acc;
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], x[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], x[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], x[0], c, 0, 0, 0);
-        acc = c;
-    };
-
-    f32x16 acc[2][2];
-    const int chunks = p.C / 16;
-    setup(tile);
-    load(0, (tile % p.gn) * HC_BN);
-    for (;;) {
-        const int m_blk = tile / p.gn * 512;
-        const int n_blk = (tile % p.gn) * HC_BN;
-        const int next = tile + per_xcd;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-        for (int j = 0; j < chunks; ++j) {
-            __builtin_amdgcn_s_barrier();             // every wave is done reading chunk j-1
-            asm volatile("" ::: "memory");
-            store();
-            if (j + 1 < chunks) {
-                load(j + 1, n_blk);
-            } else if (next < t_end) {                // the next tile's first chunk flies over this
-                setup(next);                          // chunk's MFMAs and the epilogue
-                load(0, (next % p.gn) * HC_BN);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            // 9 taps x 4 (pixel, channel) fragment pairs; each operand is re-read for the next tap
-            // as soon as its last MFMA of this tap has issued (no extra registers)
-            bf16x8_t fx0[3], fx1[3], fw0[3], fw1[3];
-            rd_x(0, 0, fx0);
-            rd_w(0, 0, fw0);
-            rd_w(0, 1, fw1);
-            rd_x(0, 1, fx1);
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                mm6(fw0, fx0, acc[0][0]);
-                mm6(fw1, fx0, acc[0][1]);
-                if (t + 1 < 9) rd_x(t + 1, 0, fx0);
-                __builtin_amdgcn_sched_barrier(0);
-                mm6(fw0, fx1, acc[1][0]);
-                if (t + 1 < 9) rd_w(t + 1, 0, fw0);
-                __builtin_amdgcn_sched_barrier(0);
-                mm6(fw1, fx1, acc[1][1]);
-                if (t + 1 < 9) {
-                    rd_w(t + 1, 1, fw1);
-                    rd_x(t + 1, 1, fx1);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        epilogue<512, HC_BN, 8, 1>(p, acc, m_blk, n_blk, wave, 0, lr, lh);
-        if (next >= t_end) break;
-        tile = next;
-    }
-}
-
 // packed fp32 weight [n][k_pad] -> [k_pad/16][q][n][8] bf16 planes, q = plane*2 + (k%16)/8,
 // plane 0/1/2 = hi/mid/lo of the round-to-nearest split (exact: hi + mid + lo == w)
 __global__ void split_weight6_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int n, int k_pad) {
@@ -1509,33 +1294,6 @@ static bool lean_ok(const pu_conv_args* a) {
     if ((long long)a->k_pad * a->n * 12 >= (1LL << 31)) return false;
     return true;
 }
-// compute units of the current device (cached per device)
-static int device_cus() {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        int n = 0;
-        cus[dev] = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8) ? n : 256;
-    }
-    return cus[dev];
-}
-
-// the halo kernel: 3x3 / s1 / p1 same-size convolutions on x6 operands, width 32/64/128, whole
-// 512-pixel row blocks, 16-channel chunks of one source, 64-channel output tiles
-static bool halo_ok(const pu_conv_args* a) {
-    if (!uses_x6(a) || (a->flags & (PU_EPI_SHUFFLE2 | PU_CONV_NO_HALO)) || !vec_epilogue(a)) return false;
-    const int C = a->c0 + a->c1;
-    if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1) return false;
-    if (a->in_h != a->out_h || a->in_w != a->out_w) return false;
-    if (!(a->out_w == 32 || a->out_w == 64 || a->out_w == 128) || a->out_h % (512 / a->out_w)) return false;
-    if (!(a->cgroup == 16 || a->cgroup == 32) || a->c0 % a->cgroup || a->c1 % a->cgroup) return false;
-    if (a->k_pad != 9 * C || a->n % HC_BN) return false;
-    if ((long long)a->batch * a->in_h * a->in_w * (a->c0 > a->c1 ? a->c0 : a->c1) >= (1LL << 31)) return false;
-    if ((long long)a->k_pad * a->n * 6 >= (1LL << 31)) return false;
-    return true;
-}
-
 static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
     if (!uses_x6(a)) {
         choose_tile(M, a->n, bm, bn);
@@ -1683,21 +1441,6 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
 #undef PU_SC
         return check_launch("pu_conv_igemm (small-channel)");
     }
-    if (halo_ok(a)) {
-        PU_REQUIRE(((uintptr_t)a->weight6 & 15) == 0, "pu_conv_igemm: weight6 must be 16-byte aligned");
-        p.wt = reinterpret_cast<const float*>(a->weight6);
-        p.ksplit = 1;
-        p.gn = N / HC_BN;
-        // persistent: one block per CU (142 KB of LDS), 8 XCD tile ranges
-        const long long tiles = M / 512 * p.gn;
-        const long long per_xcd = ceil_div(tiles, 8LL);
-        const int cu_per_xcd = device_cus() / 8;
-        const dim3 hgrid((unsigned)(8 * (per_xcd < cu_per_xcd ? per_xcd : cu_per_xcd)));
-        if (a->out_w == 128) hipLaunchKernelGGL((igemm_halo_x6_kernel<128>), hgrid, dim3(HC_NT), 0, s, p);
-        else if (a->out_w == 64) hipLaunchKernelGGL((igemm_halo_x6_kernel<64>), hgrid, dim3(HC_NT), 0, s, p);
-        else hipLaunchKernelGGL((igemm_halo_x6_kernel<32>), hgrid, dim3(HC_NT), 0, s, p);
-        return check_launch("pu_conv_igemm (x6 halo)");
-    }
     int bm, bn;
     plan_tiles(a, M, &bm, &bn, &p.ksplit, &p.t_per);
     p.gn = ceil_div(N, bn);
@@ -1768,7 +1511,7 @@ extern "C" int pu_split_weight6(const float* packed, void* out, int n, int k_pad
 extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
     if (!a || a->batch <= 0 || a->out_h <= 0 || a->out_w <= 0 || a->n <= 0 || a->k_pad <= 0) return 0;
     const long long M = (long long)a->batch * a->out_h * a->out_w;
-    if (small_conv_ok(a) || stem_conv_ok(a) || halo_ok(a)) return 0;
+    if (small_conv_ok(a) || stem_conv_ok(a)) return 0;
     int bm, bn, ks, tp;
     plan_tiles(a, M, &bm, &bn, &ks, &tp);
     return split_bytes(M, a->n, ks);
@@ -1785,13 +1528,6 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         *bm = ST_TH * ST_TW;
         *bn = a->n;
         *mode = 5;
-        if (ksplit) *ksplit = 1;
-        return PU_OK;
-    }
-    if (halo_ok(a)) {                // reported as mode 6 ("halo,x6"), 512 pixels x 64 channels
-        *bm = 512;
-        *bn = HC_BN;
-        *mode = 6;
         if (ksplit) *ksplit = 1;
         return PU_OK;
     }

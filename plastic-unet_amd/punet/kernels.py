@@ -10,7 +10,7 @@ import torch
 
 from . import _lib
 from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, check,
-                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO)
+                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
@@ -23,24 +23,12 @@ def lib():
 
 # ------------------------------------------------------------------------------ launch profiler
 _PROF = None
-_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem", 6: "halo,x6"}
+_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem"}
 
 # fp32 GEMM arithmetic of the MFMA convolutions: "split6" (default) = each fp32 product as 6 exact
 # bf16 products on the bf16 MFMA pipe (pu_split_weight6 / pu_conv_args.weight6, fp32-accurate);
 # "native" = v_mfma_f32_32x32x2_f32.  Read when a weight is packed and when a conv launches.
 _FP32_MATH = os.environ.get("PU_FP32_MATH", "split6")
-
-
-# 3x3/s1 convolutions of width 32/64/128 on the halo kernel (default) or the per-tap lean kernel
-# (PU_CONV_HALO=0: A/B runs; tests flip it with set_conv_halo)
-_CONV_HALO = os.environ.get("PU_CONV_HALO", "1") != "0"
-
-
-def set_conv_halo(on):
-    """Route eligible convolutions to the halo kernel (True) or the per-tap kernel.  Returns the previous setting."""
-    global _CONV_HALO
-    prev, _CONV_HALO = _CONV_HALO, bool(on)
-    return prev
 
 
 def fp32_math():
@@ -165,7 +153,7 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
         _req(t, nm, dt)
     _req(bias, "bias")
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
-        | (PU_EPI_RESID if resid is not None else 0) | (0 if _CONV_HALO else PU_CONV_NO_HALO)
+        | (PU_EPI_RESID if resid is not None else 0)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,

@@ -131,24 +131,3 @@ def test_trunk_parameter_order_covers_every_trunk_parameter():
         head = {id(m.w), id(m.alpha), id(m.eta)}
         assert trunk | head == {id(p) for p in m.parameters()}
         assert len(t.params) == 4 * depth + 6 * (depth - 1) + 2
-
-
-def test_halo_kernel_is_dispatched():
-    """the shapes above really take the halo kernel (pu_conv_igemm_tile mode 6)"""
-    import ctypes
-    from punet import kernels as K
-    from punet._lib import ConvArgs
-    L = K.lib()
-    for (B, H, W, c0, c1, n) in ((2, 8, 128, 16, 16, 64), (32, 64, 64, 128, 0, 128), (32, 32, 32, 256, 256, 256)):
-        C = c0 + c1
-        cg = K.cgroup_for(c0, c1)
-        a = ConvArgs(B, H, W, H, W, 3, 3, 1, 1, 1, c0, 1 if c1 else None, c1, 16, 9 * C, cg, n, None,
-                     16, n, None, None, None, 0, None, 0, None, 0, 0, 0)
-        a.weight6 = 16
-        bm, bn, mode, ks = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        assert L.pu_conv_igemm_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(mode),
-                                    ctypes.byref(ks)) == 0
-        assert (mode.value, bm.value, bn.value) == (6, 512, 64), (B, H, W, c0, c1, n, mode.value)
-        a.flags = 16                     # PU_CONV_NO_HALO: the per-tap kernel
-        L.pu_conv_igemm_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(mode), ctypes.byref(ks))
-        assert mode.value == 4
