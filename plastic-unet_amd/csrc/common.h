@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdarg.h>
+#include <type_traits>
 
 #include "plastic_unet.h"
 
@@ -88,6 +89,33 @@ __device__ __forceinline__ int xcd_remap(int b, int total) {
     const int xcd = b & 7, local = b >> 3;
     const int q = total >> 3, r = total & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
+
+// compile-time loop: f(integral_constant<int, I>) for I = 0 .. N-1 (unrolled; I usable as a constant)
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, F, I + 1>(static_cast<F&&>(f));
+    }
+}
+// lean implicit-GEMM loaders: an out-of-image tap gets this byte offset, outside every buffer
+// descriptor's range, so the range check writes zeros into LDS (probed: tools/probes/oob_lds.hip)
+constexpr unsigned LEAN_OOB = 0x80000000u;
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// buffer_load_dwordx4 ... lds of 16 B per lane through a descriptor built from wave-uniform
+// inputs, made provably uniform (no waterfall loops around the loads); bytes == 0 drops every
+// lane (zeros land in LDS).  Kept out of the kernel template so the host pass never sees the
+// descriptor type.
+__device__ __forceinline__ void lean_load(const void* base, unsigned bytes, void* lds_dst, unsigned voff, unsigned soff) {
+    const unsigned long long b = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_dst, 16, voff, __builtin_amdgcn_readfirstlane(soff), 0, 0);
 }
 
 }  // namespace pu

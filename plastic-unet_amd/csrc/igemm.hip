@@ -781,16 +781,8 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
 // Requirements (host: lean_ok): 3x3 taps, K order cgroup 16 (CG 1) or 32 (CG 2), c1 == 0 or
 // c1 == c0 (one pixel stride for both sources), K == k_pad, split-K on group boundaries,
 // every tensor under 2 GB.
-template <int N, typename F, int I = 0>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<N, F, I + 1>(static_cast<F&&>(f));
-    }
-}
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-constexpr unsigned LEAN_OOB = 0x80000000u;
 
 __device__ __forceinline__ unsigned pk_bf16(f32x2 v) {
     const bf16x2_t h = __builtin_convertvector(v, bf16x2_t);
@@ -818,19 +810,6 @@ __device__ __forceinline__ void split3_pairs(const f32x4 lo4, const f32x4 hi4, b
     h = __builtin_bit_cast(bf16x8_t, hv);
     m = __builtin_bit_cast(bf16x8_t, mv);
     l = __builtin_bit_cast(bf16x8_t, lv);
-}
-
-// buffer_load_dwordx4 ... lds of 16 B per lane through a descriptor built from wave-uniform
-// inputs, made provably uniform (no waterfall loops around the loads); bytes == 0 drops every
-// lane (zeros land in LDS).  Kept out of the kernel template so the host pass never sees the
-// descriptor type.
-__device__ __forceinline__ void lean_load(const void* base, unsigned bytes, void* lds_dst, unsigned voff, unsigned soff) {
-    const unsigned long long b = (unsigned long long)base;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
-    void* ub = (void*)(((unsigned long long)hi << 32) | lo);
-    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_dst, 16, voff, __builtin_amdgcn_readfirstlane(soff), 0, 0);
 }
 
 template <int BM, int BN, int WM, int WN, int NW, int CG>

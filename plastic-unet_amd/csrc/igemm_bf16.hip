@@ -40,6 +40,7 @@ struct IgemmBf16Params {
     float* part;
     int shuf_h, shuf_w, shuf_off;
     FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
+    int in_pix;             // batch * Hi * Wi (the lean kernel's buffer extent)
 };
 
 struct EpiRowB {
@@ -279,6 +280,197 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(const IgemmBf16Params p
     }
 }
 
+// ---------------------------------------------------------------- lean bf16 kernel
+// The loader of igemm.hip's lean x6 kernel on bf16 operands: buffer_load ... lds through buffer
+// descriptors, per-lane byte offsets precomputed once per block for all 9 taps (an out-of-image
+// tap gets LEAN_OOB and lands as zeros), the stage's (tap, channel) offset one scalar soffset, the
+// 9 taps of a 32-channel group unrolled (ring slots and LDS addresses are immediates).  A stage is
+// one (tap, 32-channel) K slice in 64-B LDS rows with igemm_bf16_kernel's swizzle; 2 x FM x FN
+// MFMAs per wave per stage, one barrier per stage.  Tiles 256 x 128 (2 x 2 waves, 16 MFMAs per
+// stage) and 256 x 64 (4 x 1).  Requirements (host: lean_ok_b): 3x3, cgroup 32, c1 == 0 or
+// c1 == c0, K == k_pad, split-K on group boundaries, every tensor under 2 GB.
+template <int BM, int BN, int WM, int WN, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void igemm_bf16_lean_kernel(const IgemmBf16Params p) {
+    constexpr int FM = BM / WM / 32;
+    constexpr int FN = BN / WN / 32;
+    constexpr int A_LD = BM / (16 * NW);
+    constexpr int B_LD = BN / (16 * NW);
+    constexpr int G = A_LD + B_LD;
+    constexpr int STAGE = (BM + BN) * BK16;   // bf16 elements per ring slot
+    constexpr int SPG = 9;                     // stages per 32-channel group (taps)
+    static_assert(WM * WN == NW && A_LD >= 1 && B_LD >= 1, "lean bf16 tile");
+
+    __shared__ __attribute__((aligned(16))) __bf16 lds[3 * STAGE];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int lr = lane & 31, lh = lane >> 5;
+    int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int kz = tile / (gridDim.x / p.ksplit);
+    tile -= kz * (gridDim.x / p.ksplit);
+    const int mb = tile / p.gn;
+    const int m_blk = mb * BM;
+    const int n_blk = (tile - mb * p.gn) * BN;
+
+    const int cs = p.c0;                                      // == c1 when c1 != 0
+    const int shift = p.pad * p.Wi + p.pad;
+    const unsigned a_bytes0 = (unsigned)(((long long)p.in_pix + shift) * cs * 2);
+    const __bf16* a0p = p.src0 - (long long)shift * cs;
+    const __bf16* a1p = (p.c1 ? p.src1 : p.src0) - (long long)shift * cs;
+    const unsigned w_bytes = (unsigned)((long long)p.k_pad * p.N * 2);
+
+    const int lq = lane >> 2;
+    const int kc = (lane & 3) ^ ((lane >> 4) & 3);   // logical 16-B chunk this lane fetches
+    unsigned vbase[A_LD], vmask[A_LD];               // row byte offset, in-image taps (bit r*3+q)
+#pragma unroll
+    for (int j = 0; j < A_LD; ++j) {
+        const int m = m_blk + wave * (BM / NW) + 16 * j + lq;
+        int hb = 0, wb = 0, pix = 0;
+        const bool mv = m < p.M;
+        if (mv) {
+            const int t = fdiv(m, p.dWo);
+            const int wo = m - t * p.Wo;
+            const int b = fdiv(t, p.dHo);
+            const int ho = t - b * p.Ho;
+            hb = ho * p.stride - p.pad;
+            wb = wo * p.stride - p.pad;
+            pix = (b * p.Hi + hb) * p.Wi + wb + shift;
+        }
+        vbase[j] = (unsigned)pix * (unsigned)(cs * 2) + kc * 16;
+        unsigned msk = 0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (mv && (unsigned)(hb + r) < (unsigned)p.Hi && (unsigned)(wb + q) < (unsigned)p.Wi) msk |= 1u << (r * 3 + q);
+        vmask[j] = msk;
+    }
+    unsigned tapoff[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) tapoff[r * 3 + q] = (unsigned)((r * p.Wi + q) * cs * 2);
+    unsigned wv[B_LD];
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) {
+        const int n = n_blk + wave * (BN / NW) + 16 * j + lq;
+        wv[j] = n < p.N ? (unsigned)(n * p.k_pad * 2 + kc * 16) : LEAN_OOB;
+    }
+
+    const int groups = p.k_pad / (BK16 * SPG);
+    const int gps = p.t_per / SPG;                  // groups per split
+    const int g0 = kz * gps;
+    const int g1 = min(groups, g0 + gps);
+
+    auto issue = [&](int g, auto uc) {
+        constexpr int u = decltype(uc)::value;      // tap
+        const bool live = g < g1;
+        const int c = g * BK16;
+        const bool second = c >= p.c0;
+        const __bf16* abase = second ? a1p : a0p;
+        const unsigned soff = tapoff[u] + (unsigned)((second ? c - p.c0 : c) * 2);
+        __bf16* a_slot = lds + (u % 3) * STAGE;
+        __bf16* b_slot = a_slot + BM * BK16;
+#pragma unroll
+        for (int j = 0; j < A_LD; ++j)
+            lean_load(abase, live ? a_bytes0 : 0u, a_slot + (wave * (BM / NW) + 16 * j) * BK16,
+                      ((vmask[j] >> u) & 1u) ? vbase[j] : LEAN_OOB, soff);
+        const unsigned wsoff = (unsigned)(g * SPG + u) * (BK16 * 2);
+#pragma unroll
+        for (int j = 0; j < B_LD; ++j)
+            lean_load(p.wt, live ? w_bytes : 0u, b_slot + (wave * (BN / NW) + 16 * j) * BK16, wv[j], wsoff);
+    };
+
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int a_row0 = wm * (BM / WM) + lr;
+    const int b_row0 = wn * (BN / WN) + lr;
+    const int swz = (lr >> 2) & 3;
+
+    if (g0 < g1) {
+        issue(g0, std::integral_constant<int, 0>{});
+        issue(g0, std::integral_constant<int, 1>{});
+    }
+    for (int g = g0; g < g1; ++g) {
+        static_for<SPG>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const __bf16* a = lds + (u % 3) * STAGE;
+            const __bf16* b = a + BM * BK16;
+            bf16x8 fa[2][FM], fb[2][FN];
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const int pos = ((kk * 2 + lh) ^ swz) * 8;
+#pragma unroll
+                for (int i = 0; i < FM; ++i) fa[kk][i] = *reinterpret_cast<const bf16x8*>(a + (a_row0 + i * 32) * BK16 + pos);
+#pragma unroll
+                for (int j = 0; j < FN; ++j) fb[kk][j] = *reinterpret_cast<const bf16x8*>(b + (b_row0 + j * 32) * BK16 + pos);
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+                for (int i = 0; i < FM; ++i)
+#pragma unroll
+                    for (int j = 0; j < FN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[kk][j], fa[kk][i], acc[i][j], 0, 0, 0);
+                if (kk == 0) {
+                    if constexpr (u + 2 < SPG) issue(g, std::integral_constant<int, u + 2>{});
+                    else issue(g + 1, std::integral_constant<int, u + 2 - SPG>{});
+                }
+            }
+        });
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if (p.ksplit > 1) {
+        float* part = p.part + (long long)kz * p.M * p.N;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+            if (m >= p.M) continue;
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                    if (n >= p.N) continue;
+                    f32x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                    *reinterpret_cast<f32x4*>(part + (long long)m * p.N + n) = v;
+                }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
+        if (m >= p.M) continue;
+        const EpiRowB er = epi_row_b(p, m);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int n = n_blk + wn * (BN / WN) + j * 32 + 8 * q + 4 * lh;
+                if (n >= p.N) continue;
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                epi_store4_b(p, er, n, v);
+            }
+    }
+}
+
 __global__ __launch_bounds__(256) void igemm_bf16_splitk_epilogue_kernel(const IgemmBf16Params p) {
     const int nq = p.N >> 2;
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -317,6 +509,37 @@ static void plan_split_b(const pu_conv_args* a, long long M, int bm, int bn, int
     if (ks > T / 4) ks = T / 4;
     if (ks < 2) return;
     *t_per = ceil_div(T, ks);
+    *ksplit = ceil_div(T, *t_per);
+}
+
+// the lean kernel: 3x3, 32-channel K groups, one pixel stride for both sources, K == k_pad,
+// byte offsets within 2 GB
+static bool lean_ok_b(const pu_conv_args* a) {
+    const int C = a->c0 + a->c1;
+    if (a->kh != 3 || a->kw != 3 || a->cgroup != 32) return false;
+    if (a->c1 != 0 && a->c1 != a->c0) return false;
+    if (a->k_pad != 9 * C || (a->flags & PU_EPI_SHUFFLE2)) return false;
+    const long long shift = (long long)a->pad * a->in_w + a->pad;
+    if (((long long)a->batch * a->in_h * a->in_w + shift) * a->c0 * 2 >= (1LL << 31)) return false;
+    if ((long long)a->k_pad * a->n * 2 >= (1LL << 31)) return false;
+    return true;
+}
+
+// lean tiles: 256 x 128 (N > 64) or 256 x 64, 4 waves, ~2 resident blocks per CU (72 / 61 KB of
+// LDS); small pixel grids split K on group boundaries until ~2 blocks per CU
+static void plan_lean_b(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
+    *bm = 256;
+    *bn = a->n > 64 ? 128 : 64;
+    const int T = a->k_pad / BK16;
+    *ksplit = 1;
+    *t_per = T;
+    const int tiles = blocks_for_b(M, a->n, *bm, *bn);
+    const int target = 512;
+    if (tiles >= target - target / 16) return;
+    int ks = ceil_div(target, tiles);
+    if (ks > T / 9) ks = T / 9;
+    if (ks < 2) return;
+    *t_per = ceil_div(ceil_div(T, ks), 9) * 9;
     *ksplit = ceil_div(T, *t_per);
 }
 
@@ -361,6 +584,7 @@ static int setup_bf16(const pu_conv_args* a, IgemmBf16Params* pp, long long* Mou
     p.dWo = make_fastdiv(a->out_w); p.dHo = make_fastdiv(a->out_h);
     p.dC = make_fastdiv(C); p.dKw = make_fastdiv(a->kw); p.dCo = make_fastdiv(shuffle ? a->n / 4 : 1);
     p.dTaps = make_fastdiv(p.taps);
+    p.in_pix = a->batch * a->in_h * a->in_w;
     *Mout = M;
     return PU_OK;
 }
@@ -374,8 +598,12 @@ extern "C" size_t pu_conv_igemm_bf16_workspace_bytes(const pu_conv_args* a) {
     long long M;
     if (setup_bf16(a, &p, &M) != PU_OK) return 0;
     int bm, bn, ks, tp;
-    choose_tile_b(M, a->n, &bm, &bn);
-    plan_split_b(a, M, bm, bn, &ks, &tp);
+    if (lean_ok_b(a)) {
+        plan_lean_b(a, M, &bm, &bn, &ks, &tp);
+    } else {
+        choose_tile_b(M, a->n, &bm, &bn);
+        plan_split_b(a, M, bm, bn, &ks, &tp);
+    }
     return ks > 1 ? (size_t)ks * (size_t)M * (size_t)a->n * sizeof(float) : 0;
 }
 
@@ -386,9 +614,14 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
     if (st != PU_OK) return st;
     const int N = a->n;
     int bm, bn;
-    choose_tile_b(M, N, &bm, &bn);
+    const bool lean = lean_ok_b(a);
+    if (lean) {
+        plan_lean_b(a, M, &bm, &bn, &p.ksplit, &p.t_per);
+    } else {
+        choose_tile_b(M, N, &bm, &bn);
+        plan_split_b(a, M, bm, bn, &p.ksplit, &p.t_per);
+    }
     p.gn = ceil_div(N, bn);
-    plan_split_b(a, M, bm, bn, &p.ksplit, &p.t_per);
     if (p.ksplit > 1 && (!a->workspace || a->ws_bytes < (size_t)p.ksplit * M * N * sizeof(float))) {
         p.ksplit = 1;
         p.t_per = a->k_pad / BK16;
@@ -396,7 +629,9 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
     p.part = (float*)a->workspace;
     hipStream_t s = as_stream(stream);
     const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
-    if (bm == 256) hipLaunchKernelGGL((igemm_bf16_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
+    if (lean && bn == 128) hipLaunchKernelGGL((igemm_bf16_lean_kernel<256, 128, 2, 2, 4>), grid, dim3(256), 0, s, p);
+    else if (lean) hipLaunchKernelGGL((igemm_bf16_lean_kernel<256, 64, 4, 1, 4>), grid, dim3(256), 0, s, p);
+    else if (bm == 256) hipLaunchKernelGGL((igemm_bf16_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
     else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_bf16_kernel<128, 128, 2, 2, 3>), grid, dim3(256), 0, s, p);
     else if (bm == 128) hipLaunchKernelGGL((igemm_bf16_kernel<128, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((igemm_bf16_kernel<64, 64, 2, 2, 3>), grid, dim3(256), 0, s, p);
@@ -412,9 +647,13 @@ extern "C" int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, 
     long long M;
     int st = setup_bf16(a, &p, &M);
     if (st != PU_OK) return st;
-    choose_tile_b(M, a->n, bm, bn);
     int ks, tp;
-    plan_split_b(a, M, *bm, *bn, &ks, &tp);
+    if (lean_ok_b(a)) {
+        plan_lean_b(a, M, bm, bn, &ks, &tp);
+    } else {
+        choose_tile_b(M, a->n, bm, bn);
+        plan_split_b(a, M, *bm, *bn, &ks, &tp);
+    }
     if (ksplit) *ksplit = (ks > 1 && a->workspace && a->ws_bytes >= (size_t)ks * M * a->n * sizeof(float)) ? ks : 1;
     return PU_OK;
 }
