@@ -92,7 +92,10 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
  *   over ksplit blocks per tile; the partial tiles go to the workspace and a second kernel sums
  *   them in fixed split order (deterministic) and runs the epilogue above.  NULL -> no split.
  * ------------------------------------------------------------------------------------------- */
-enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8 };
+/* PU_CONV_NO_HALO: a dispatch hint, not an epilogue flag - keep a bf16 3x3/s1 layer that the halo
+ * kernel would take (width 32/64/128) on the per-tap lean kernel (A/B runs and the bit-identity
+ * test: both compute the same sums in the same order when the per-tap launch is not split) */
+enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8, PU_CONV_NO_HALO = 16 };
 
 typedef struct {
     int batch;
@@ -276,7 +279,9 @@ int pu_outconv_bwd(const float* x, const float* w, const float* dy, float* dx, f
  * ------------------------------------------------------------------------------------------- */
 int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream);
 size_t pu_conv_igemm_bf16_workspace_bytes(const pu_conv_args* a);
-int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit);
+/* the bf16 kernel pu_conv_igemm_bf16 would launch: tile bm x bn, K splits, kind 0 = tile kernel,
+ * 1 = lean per-tap kernel, 2 = halo kernel (kind may be NULL) */
+int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit, int* kind);
 size_t pu_wgrad_bf16_workspace_bytes(const pu_wgrad_args* a);
 int pu_wgrad_bf16(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);
 int pu_wgrad_bf16_phase(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, int phase, void* stream);

@@ -471,6 +471,184 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
 }
 
+// ---------------------------------------------------------------- halo bf16 kernel
+// 3x3 / stride 1 / pad 1 convolutions (fwd and dgrad) of width W = 32, 64 or 128: the lean
+// kernel re-reads every input pixel from L2 once per tap (9 x 64 B per pixel and 32-channel group,
+// ~2x the L2->LDS rate the MFMAs could consume at bf16); this one loads the (R+2) x (W+2) halo of
+// R = 256 / W output rows once per group and serves all 9 taps from LDS.
+//   block: 256 output pixels (R whole rows of one image) x 64 output channels, 4 waves of 64 x 64
+//   (2 x 2 fragments, 72 MFMAs per wave per group); persistent over an XCD-contiguous tile range;
+//   LDS (single image, 2 blocks per CU): the halo as [pixel][32 channels] with an 80-B pixel
+//   stride (5 bank quads: conflict-free 16-B fragment reads at every tap shift, every address one
+//   base register + an immediate) and the group's 9 tap slices of the weights [tap][n][64 B]
+//   (16-B chunks swizzled by n bits 2-3); the next group's halo and weights are loaded into
+//   registers under the current group's MFMAs and stored between two barriers.
+// K order (cgroup 32) and the MFMA order per accumulator are igemm_bf16_lean_kernel's, so the
+// two are bit-identical.  Requirements (host: halo_ok_b).
+constexpr int HB_NT = 256;
+constexpr int HB_BN = 64;
+constexpr int HB_PX = 80;
+
+template <int W>
+__global__ __launch_bounds__(HB_NT) __attribute__((amdgpu_waves_per_eu(2))) void igemm_bf16_halo_kernel(const IgemmBf16Params p) {
+    constexpr int R = 256 / W;
+    constexpr int HW = W + 2;
+    constexpr int HP = (R + 2) * HW;                  // halo pixels
+    constexpr int XB = HP * HB_PX;
+    constexpr int WB = 9 * HB_BN * 64;
+    constexpr int ITEMS = 4 * HP;                     // (pixel, 16-B chunk) pieces
+    constexpr int IT = (ITEMS + HB_NT - 1) / HB_NT;
+    constexpr int WPC = 9 * HB_BN * 4;                // 16-B weight pieces per group
+    constexpr int WIT = (WPC + HB_NT - 1) / HB_NT;
+    static_assert(R * W == 256 && W % 32 == 0, "halo tile");
+
+    __shared__ __attribute__((aligned(16))) char lds[XB + WB];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const int ntiles = p.M / 256 * p.gn;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
+    const int tq = (ntiles + 7) >> 3;
+    const int t_end = min(ntiles, (xcd + 1) * tq);
+    int tile = xcd * tq + (int)(blockIdx.x >> 3);
+    if (tile >= t_end) return;                        // uniform per block
+    const int rb = p.Ho / R;
+
+    int xsrc[IT];                                     // source element offset (-1: padding)
+    auto setup = [&](int t) {
+        const int mt = t / p.gn;
+        const int b = mt / rb;
+        const int r0 = (mt - b * rb) * R;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int e = it * HB_NT + tid;
+            const int hp = e >> 2;
+            const int hr = hp / HW, hc = hp - hr * HW;
+            const int ir = r0 - 1 + hr, ic = hc - 1;
+            const bool ok = e < ITEMS && (unsigned)ir < (unsigned)p.Hi && (unsigned)ic < (unsigned)W;
+            xsrc[it] = ok ? ((b * p.Hi + ir) * W + ic) : -1;
+        }
+    };
+
+    f32x4 xr[IT], wr[WIT];
+    auto load = [&](int g, int n_blk) {
+        const int c = g * 32;
+        const bool second = c >= p.c0;
+        const __bf16* src = second ? p.src1 : p.src0;
+        const int cs = second ? p.c1 : p.c0;
+        const int cc = (second ? c - p.c0 : c) + (tid & 3) * 8;
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            xr[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (xsrc[it] >= 0) xr[it] = *reinterpret_cast<const f32x4*>(src + xsrc[it] * cs + cc);
+        }
+        const __bf16* wsrc = p.wt + (long long)n_blk * p.k_pad + g * 9 * 32;
+#pragma unroll
+        for (int w = 0; w < WIT; ++w) {
+            const int e = w * HB_NT + tid;
+            if (e < WPC) {
+                const int ch = e & 3, n = (e >> 2) & 63, tap = e >> 8;
+                wr[w] = *reinterpret_cast<const f32x4*>(wsrc + n * p.k_pad + tap * 32 + ch * 8);
+            }
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int e = it * HB_NT + tid;
+            if (e < ITEMS) *reinterpret_cast<f32x4*>(lds + (e >> 2) * HB_PX + (e & 3) * 16) = xr[it];
+        }
+#pragma unroll
+        for (int w = 0; w < WIT; ++w) {
+            const int e = w * HB_NT + tid;
+            if (e < WPC) {
+                const int ch = e & 3, n = (e >> 2) & 63, tap = e >> 8;
+                *reinterpret_cast<f32x4*>(lds + XB + (tap * HB_BN + n) * 64 + ((ch ^ ((n >> 2) & 3)) << 4)) = wr[w];
+            }
+        }
+    };
+
+    // wave = 64 output pixels (fragments i = 0, 1 of 32) x 64 channels (fragments j = 0, 1)
+    const int p0 = wave * 64;
+    const int orow = p0 / W, ocol = p0 - orow * W;
+    const unsigned xa = (unsigned)((orow * HW + ocol + lr) * HB_PX);
+    constexpr int FRAG1 = (32 / W) * HW + (32 % W);   // halo pixels from fragment 0 to 1
+    const unsigned wa = (unsigned)(XB + lr * 64);
+    const int wsw = (lr >> 2) & 3;
+
+    f32x16 acc[2][2];
+    const int chunks = p.C / 32;
+    setup(tile);
+    load(0, (tile % p.gn) * HB_BN);
+    for (;;) {
+        const int m_blk = tile / p.gn * 256;
+        const int n_blk = (tile % p.gn) * HB_BN;
+        const int next = tile + per_xcd;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int g = 0; g < chunks; ++g) {
+            __builtin_amdgcn_s_barrier();             // every wave is done reading group g-1
+            asm volatile("" ::: "memory");
+            store();
+            if (g + 1 < chunks) {
+                load(g + 1, n_blk);
+            } else if (next < t_end) {                // the next tile's first group flies over
+                setup(next);                          // this group's MFMAs and the epilogue
+                load(0, (next % p.gn) * HB_BN);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int toff = ((t / 3) * HW + (t % 3)) * HB_PX;
+                bf16x8 fx[2][2], fw[2][2];
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) {
+                    const int chk = kk * 2 + lh;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        fx[kk][i] = *reinterpret_cast<const bf16x8*>(lds + xa + toff + i * FRAG1 * HB_PX + chk * 16);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        fw[kk][j] = *reinterpret_cast<const bf16x8*>(lds + wa + (t * HB_BN + j * 32) * 64 + ((chk ^ wsw) << 4));
+                }
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[kk][j], fx[kk][i], acc[i][j], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = m_blk + p0 + i * 32 + lr;
+            const EpiRowB er = epi_row_b(p, m);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int n = n_blk + j * 32 + 8 * q + 4 * lh;
+                    f32x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                    epi_store4_b(p, er, n, v);
+                }
+        }
+        if (next >= t_end) break;
+        tile = next;
+    }
+}
+
 __global__ __launch_bounds__(256) void igemm_bf16_splitk_epilogue_kernel(const IgemmBf16Params p) {
     const int nq = p.N >> 2;
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -510,6 +688,30 @@ static void plan_split_b(const pu_conv_args* a, long long M, int bm, int bn, int
     if (ks < 2) return;
     *t_per = ceil_div(T, ks);
     *ksplit = ceil_div(T, *t_per);
+}
+
+// the halo kernel: 3x3 / s1 / p1 same-size, width 32 / 64 / 128, whole 256-pixel row blocks,
+// 32-channel groups, 64-channel output tiles, plain (non-SHUFFLE2) epilogue
+static bool halo_ok_b(const pu_conv_args* a) {
+    const int C = a->c0 + a->c1;
+    if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1 || a->cgroup != 32) return false;
+    if (a->in_h != a->out_h || a->in_w != a->out_w || (a->flags & (PU_EPI_SHUFFLE2 | PU_CONV_NO_HALO))) return false;
+    if (!(a->out_w == 32 || a->out_w == 64 || a->out_w == 128) || a->out_h % (256 / a->out_w)) return false;
+    if (a->k_pad != 9 * C || a->n % HB_BN) return false;
+    if ((long long)a->batch * a->in_h * a->in_w * (a->c0 > a->c1 ? a->c0 : a->c1) >= (1LL << 31)) return false;
+    if ((long long)a->k_pad * a->n >= (1LL << 31)) return false;
+    return true;
+}
+
+static int device_cus_b() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        cus[dev] = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8) ? n : 256;
+    }
+    return cus[dev];
 }
 
 // the lean kernel: 3x3, 32-channel K groups, one pixel stride for both sources, K == k_pad,
@@ -598,6 +800,7 @@ extern "C" size_t pu_conv_igemm_bf16_workspace_bytes(const pu_conv_args* a) {
     long long M;
     if (setup_bf16(a, &p, &M) != PU_OK) return 0;
     int bm, bn, ks, tp;
+    if (halo_ok_b(a)) return 0;
     if (lean_ok_b(a)) {
         plan_lean_b(a, M, &bm, &bn, &ks, &tp);
     } else {
@@ -613,6 +816,19 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
     int st = setup_bf16(a, &p, &M);
     if (st != PU_OK) return st;
     const int N = a->n;
+    hipStream_t s = as_stream(stream);
+    if (halo_ok_b(a)) {
+        p.ksplit = 1;
+        p.gn = N / HB_BN;
+        const long long tiles = M / 256 * p.gn;
+        const long long per_xcd = ceil_div(tiles, 8LL);
+        const int blocks_per_xcd = 2 * device_cus_b() / 8;   // 2 resident blocks per CU
+        const dim3 hgrid((unsigned)(8 * (per_xcd < blocks_per_xcd ? per_xcd : blocks_per_xcd)));
+        if (a->out_w == 128) hipLaunchKernelGGL((igemm_bf16_halo_kernel<128>), hgrid, dim3(HB_NT), 0, s, p);
+        else if (a->out_w == 64) hipLaunchKernelGGL((igemm_bf16_halo_kernel<64>), hgrid, dim3(HB_NT), 0, s, p);
+        else hipLaunchKernelGGL((igemm_bf16_halo_kernel<32>), hgrid, dim3(HB_NT), 0, s, p);
+        return check_launch("pu_conv_igemm_bf16 (halo)");
+    }
     int bm, bn;
     const bool lean = lean_ok_b(a);
     if (lean) {
@@ -627,7 +843,6 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
         p.t_per = a->k_pad / BK16;
     }
     p.part = (float*)a->workspace;
-    hipStream_t s = as_stream(stream);
     const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
     if (lean && bn == 128) hipLaunchKernelGGL((igemm_bf16_lean_kernel<256, 128, 2, 2, 4>), grid, dim3(256), 0, s, p);
     else if (lean) hipLaunchKernelGGL((igemm_bf16_lean_kernel<256, 64, 4, 1, 4>), grid, dim3(256), 0, s, p);
@@ -642,12 +857,20 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
     return check_launch("pu_conv_igemm_bf16");
 }
 
-extern "C" int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit) {
+extern "C" int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit, int* kind) {
     IgemmBf16Params p;
     long long M;
     int st = setup_bf16(a, &p, &M);
     if (st != PU_OK) return st;
     int ks, tp;
+    if (halo_ok_b(a)) {               // the halo kernel: 256 pixels x 64 channels, no split
+        *bm = 256;
+        *bn = HB_BN;
+        if (ksplit) *ksplit = 1;
+        if (kind) *kind = 2;
+        return PU_OK;
+    }
+    if (kind) *kind = lean_ok_b(a) ? 1 : 0;
     if (lean_ok_b(a)) {
         plan_lean_b(a, M, bm, bn, &ks, &tp);
     } else {

@@ -17,7 +17,7 @@ c_int, c_ll, c_size, c_float, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes
 c_double = ctypes.c_double
 P = ctypes.c_void_p
 
-PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID = 1, 2, 4, 8
+PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO = 1, 2, 4, 8, 16
 PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD, PU_PACK_CONVT3_FWD = 0, 1, 2, 3, 4
 PU_RULE_HEBB, PU_RULE_OJA = 0, 1
 
@@ -88,7 +88,7 @@ SIGNATURES = [
     ("pu_conv_igemm_bf16", c_int, [ctypes.POINTER(ConvArgs), P]),
     ("pu_conv_igemm_bf16_workspace_bytes", c_size, [ctypes.POINTER(ConvArgs)]),
     ("pu_conv_igemm_bf16_tile", c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(c_int), ctypes.POINTER(c_int),
-                                        ctypes.POINTER(c_int)]),
+                                        ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_wgrad_bf16_workspace_bytes", c_size, [ctypes.POINTER(WgradArgs)]),
     ("pu_wgrad_bf16", c_int, [ctypes.POINTER(WgradArgs), P, c_size, P]),
     ("pu_wgrad_bf16_phase", c_int, [ctypes.POINTER(WgradArgs), P, c_size, c_int, P]),

@@ -10,7 +10,7 @@ import torch
 
 from . import _lib
 from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, check,
-                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID)
+                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
@@ -29,6 +29,18 @@ _MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem"}
 # bf16 products on the bf16 MFMA pipe (pu_split_weight6 / pu_conv_args.weight6, fp32-accurate);
 # "native" = v_mfma_f32_32x32x2_f32.  Read when a weight is packed and when a conv launches.
 _FP32_MATH = os.environ.get("PU_FP32_MATH", "split6")
+
+
+# bf16 3x3/s1 convolutions of width 32/64/128 on the halo kernel (default) or the per-tap lean
+# kernel (PU_CONV_HALO=0: A/B runs; tests flip it with set_conv_halo)
+_CONV_HALO = os.environ.get("PU_CONV_HALO", "1") != "0"
+
+
+def set_conv_halo(on):
+    """Route eligible bf16 convolutions to the halo kernel (True) or the per-tap kernel.  Returns the previous setting."""
+    global _CONV_HALO
+    prev, _CONV_HALO = _CONV_HALO, bool(on)
+    return prev
 
 
 def fp32_math():
@@ -153,7 +165,7 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
         _req(t, nm, dt)
     _req(bias, "bias")
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
-        | (PU_EPI_RESID if resid is not None else 0)
+        | (PU_EPI_RESID if resid is not None else 0) | (0 if _CONV_HALO else PU_CONV_NO_HALO)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,
@@ -198,10 +210,11 @@ def _igemm_bf16(L, a, batch, out_hw, k, c0, c1, n, dst0):
     if _PROF is None:
         check(L.pu_conv_igemm_bf16(ctypes.byref(a), _stream()), "pu_conv_igemm_bf16")
         return
-    bm, bn, ks = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    L.pu_conv_igemm_bf16_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(ks))
+    bm, bn, ks, kind = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    L.pu_conv_igemm_bf16_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(ks), ctypes.byref(kind))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "igemm_bf16<%dx%d%s>" % (bm.value, bn.value, ",k%d" % ks.value if ks.value > 1 else "")
+    tag = "igemm_bf16<%dx%d%s%s>" % (bm.value, bn.value, ("", ",lean", ",halo")[kind.value],
+                                     ",k%d" % ks.value if ks.value > 1 else "")
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
         check(L.pu_conv_igemm_bf16(ctypes.byref(a), _stream()), "pu_conv_igemm_bf16")
 

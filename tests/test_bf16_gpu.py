@@ -63,7 +63,11 @@ CASES = [
     # halo-reuse wgrad (64-channel multiples, width % 16 == 0): edges, concat, odd stage counts
     (3, 7, 32, 64, 64, 64),       # 7 rows: every stage touches the top or bottom edge
     (1, 5, 48, 128, 0, 192),      # 15 stages, 2 x 3 channel tiles
-    (2, 64, 64, 64, 0, 64),       # 512 stages over 512 splits
+    (2, 64, 64, 64, 0, 64),       # 512 stages over 512 splits; halo conv (W 64, 4 row blocks)
+    # halo conv kernel (width 32/64/128, N % 64 == 0): row blocks, concat, output tiles
+    (2, 8, 128, 32, 32, 64),      # W 128: 4 row blocks per image, two sources, split dgrad output
+    (1, 16, 32, 64, 0, 128),      # W 32: 2 row blocks, 2 output-channel tiles
+    (1, 4, 128, 32, 96, 64),      # unequal concat (the per-tap lean kernel cannot take it)
 ]
 
 
@@ -180,3 +184,29 @@ def test_unetp_bf16_vs_fp64_oracle():
         num += d * d
         den += pr.grad.norm().item() ** 2
     assert (num / den) ** 0.5 < 0.15
+
+
+@pytest.mark.parametrize("c0,cout", [(32, 64), (64, 64)])
+def test_bf16_halo_conv_bit_identical_to_lean(c0, cout):
+    """the halo kernel sums the same bf16 products in the same order as the per-tap lean kernel
+    (unsplit at 8 x 128 x 128: 512 tiles), so forward and dgrad outputs are bit-identical"""
+    B, H = 8, 128
+    g = torch.Generator(device=DEV).manual_seed(c0 + cout)
+    x = torch.randn(B, H, H, c0, device=DEV, generator=g).relu().to(BF)
+    w = torch.randn(cout, c0, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    dz = torch.randn(B, H, H, cout, device=DEV, generator=g).to(BF)
+    outs = []
+    prev = K.set_conv_halo(True)
+    try:
+        for halo in (True, False):
+            K.set_conv_halo(halo)
+            pk = T._Packs()
+            y = T.conv3x3(x, w, b, pk)
+            d0, _ = T.conv3x3_dgrad(dz, w, pk, mask0=x)
+            outs.append((y, d0))
+    finally:
+        K.set_conv_halo(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--layers", default=",".join(LAYERS))
     ap.add_argument("--json", default=None)
     ap.add_argument("--ops", default="fwd,dgrad,wgrad", help="subset of fwd,dgrad,wgrad to time")
+    ap.add_argument("--bf16", action="store_true", help="bf16 activations (config C3 kernels)")
     ap.add_argument("--data", default="randn", choices=["randn", "bf16", "zeros"],
                     help="operand values (power/clock probe): bf16 = values exact in bf16 (zero mid/lo planes)")
     a = ap.parse_args()
@@ -77,6 +78,9 @@ def main():
             for t in (x0, x1, w, dz):
                 if t is not None:
                     t.copy_(t.bfloat16().float() if a.data == "bf16" else torch.zeros_like(t))
+        if a.bf16:
+            x0, dz = x0.bfloat16(), dz.bfloat16()
+            x1 = x1.bfloat16() if x1 is not None else None
         pk = T._Packs()
         flops = 2.0 * B * H * H * cout * 9 * (c0 + c1)
         r = {}
