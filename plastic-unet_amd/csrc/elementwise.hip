@@ -288,6 +288,112 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ x, const T* __restrict_
     }
 }
 
+// 16-byte vector of V = 16 / sizeof(T) channels as floats
+template <typename T>
+struct Vec16 {
+    static constexpr int V = 16 / sizeof(T);
+    float v[V];
+};
+template <typename T>
+__device__ __forceinline__ Vec16<T> ld16(const T* p) {
+    Vec16<T> r;
+    if constexpr (sizeof(T) == 4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r.v[e] = a[e];
+    } else {
+        typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+        const b8 a = *reinterpret_cast<const b8*>(p);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r.v[e] = (float)a[e];
+    }
+    return r;
+}
+template <typename T>
+__device__ __forceinline__ void st16(T* p, const float (&v)[Vec16<T>::V]) {
+    if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+        typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+        b8 a;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] = (__bf16)v[e];
+        *reinterpret_cast<b8*>(p) = a;
+    }
+}
+
+// One thread per (pooled pixel, 16-byte channel vector): even H and W, C % V == 0, 16-B aligned.
+// fwd reads the 2x2 window once (the same pool_take scan as maxpool_fwd_kernel); bwd reads the
+// window and dy once and writes all four dx pixels (zeros off the argmax / under the ReLU mask),
+// instead of one thread per full-resolution pixel re-reading the whole window.
+template <typename T>
+__global__ void maxpool_fwd_win_kernel(const T* __restrict__ x, T* __restrict__ y, int W, int C, int Ho, int Wo,
+                                       long long total) {
+    constexpr int V = Vec16<T>::V;
+    const int CV = C / V;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int cv = int(idx % CV);
+        long long t = idx / CV;
+        const int wo = int(t % Wo); t /= Wo;
+        const int ho = int(t % Ho);
+        const long long b = t / Ho;
+        const long long base = (b * 2 * Ho + 2 * ho) * (long long)W + 2 * wo;
+        float best[V];
+        int arg[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const Vec16<T> v = ld16(x + (base + (q >> 1) * W + (q & 1)) * C + cv * V);
+#pragma unroll
+            for (int e = 0; e < V; ++e) pool_take(v.v[e], q, best[e], arg[e]);
+        }
+        st16(y + idx * V, best);
+    }
+}
+
+template <typename T>
+__global__ void maxpool_bwd_win_kernel(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx, int W,
+                                       int C, int Ho, int Wo, int relu_mask, int accumulate, long long total) {
+    constexpr int V = Vec16<T>::V;
+    const int CV = C / V;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int cv = int(idx % CV);
+        long long t = idx / CV;
+        const int wo = int(t % Wo); t /= Wo;
+        const int ho = int(t % Ho);
+        const long long b = t / Ho;
+        const long long base = (b * 2 * Ho + 2 * ho) * (long long)W + 2 * wo;
+        Vec16<T> xv[4];
+        float best[V];
+        int arg[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            xv[q] = ld16(x + (base + (q >> 1) * W + (q & 1)) * C + cv * V);
+#pragma unroll
+            for (int e = 0; e < V; ++e) pool_take(xv[q].v[e], q, best[e], arg[e]);
+        }
+        const Vec16<T> g = ld16(dy + idx * V);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            T* d = dx + (base + (q >> 1) * W + (q & 1)) * C + cv * V;
+            float out[V];
+#pragma unroll
+            for (int e = 0; e < V; ++e) out[e] = (arg[e] == q && (!relu_mask || xv[q].v[e] > 0.f)) ? g.v[e] : 0.f;
+            if (accumulate) {
+                const Vec16<T> o = ld16(d);
+#pragma unroll
+                for (int e = 0; e < V; ++e) out[e] = o.v[e] + out[e];
+            }
+            st16(d, out);
+        }
+    }
+}
+
 // outconv forward: 16 lanes per pixel, each a float4 of channels; shuffle-reduce over the 16.
 template <typename T = float>
 __global__ void outconv_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
@@ -638,6 +744,12 @@ extern "C" int pu_maxpool2_fwd(const float* x, float* y, int batch, int h, int w
     PU_REQUIRE(x && y && batch > 0 && h >= 2 && w >= 2 && c > 0, "pu_maxpool2_fwd: bad args");
     const int ho = h / 2, wo = w / 2;
     const bool vec = (c % 4 == 0) && (((uintptr_t)x | (uintptr_t)y) & 15) == 0;
+    if (vec && h % 2 == 0 && w % 2 == 0) {
+        const long long wt = (long long)batch * ho * wo * (c / 4);
+        hipLaunchKernelGGL(maxpool_fwd_win_kernel<float>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream), x, y, w, c,
+                           ho, wo, wt);
+        return check_launch("pu_maxpool2_fwd");
+    }
     const long long total = (long long)batch * ho * wo * (vec ? c / 4 : c);
     if (vec)
         hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, y, h, w,
@@ -653,6 +765,12 @@ extern "C" int pu_maxpool2_bwd(const float* x, const float* dy, float* dx, int b
     PU_REQUIRE(x && dy && dx && batch > 0 && h >= 2 && w >= 2 && c > 0, "pu_maxpool2_bwd: bad args");
     const int ho = h / 2, wo = w / 2;
     const bool vec = (c % 4 == 0);
+    if (vec && h % 2 == 0 && w % 2 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) == 0) {
+        const long long wt = (long long)batch * ho * wo * (c / 4);
+        hipLaunchKernelGGL(maxpool_bwd_win_kernel<float>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream), x, dy, dx,
+                           w, c, ho, wo, relu_mask, accumulate, wt);
+        return check_launch("pu_maxpool2_bwd");
+    }
     const long long total = (long long)batch * h * w * (vec ? c / 4 : c);
     if (vec)
         hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, dy, dx,
@@ -761,6 +879,12 @@ extern "C" int pu_convert_bf16_f32(const void* x, float* y, long long n, void* s
 extern "C" int pu_maxpool2_fwd_bf16(const void* x, void* y, int batch, int h, int w, int c, void* stream) {
     PU_REQUIRE(x && y && batch > 0 && h >= 2 && w >= 2 && c > 0 && c % 4 == 0, "pu_maxpool2_fwd_bf16: bad args");
     const int ho = h / 2, wo = w / 2;
+    if (c % 8 == 0 && h % 2 == 0 && w % 2 == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
+        const long long wt = (long long)batch * ho * wo * (c / 8);
+        hipLaunchKernelGGL(maxpool_fwd_win_kernel<__bf16>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream),
+                           (const __bf16*)x, (__bf16*)y, w, c, ho, wo, wt);
+        return check_launch("pu_maxpool2_fwd_bf16");
+    }
     const long long total = (long long)batch * ho * wo * (c / 4);
     hipLaunchKernelGGL((maxpool_fwd_kernel<true, __bf16>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
                        (const __bf16*)x, (__bf16*)y, h, w, c, ho, wo, total);
@@ -771,6 +895,12 @@ extern "C" int pu_maxpool2_bwd_bf16(const void* x, const void* dy, void* dx, int
                                     int relu_mask, int accumulate, void* stream) {
     PU_REQUIRE(x && dy && dx && batch > 0 && h >= 2 && w >= 2 && c > 0 && c % 4 == 0, "pu_maxpool2_bwd_bf16: bad args");
     const int ho = h / 2, wo = w / 2;
+    if (c % 8 == 0 && h % 2 == 0 && w % 2 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) == 0) {
+        const long long wt = (long long)batch * ho * wo * (c / 8);
+        hipLaunchKernelGGL(maxpool_bwd_win_kernel<__bf16>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream),
+                           (const __bf16*)x, (const __bf16*)dy, (__bf16*)dx, w, c, ho, wo, relu_mask, accumulate, wt);
+        return check_launch("pu_maxpool2_bwd_bf16");
+    }
     const long long total = (long long)batch * h * w * (c / 4);
     hipLaunchKernelGGL((maxpool_bwd_kernel<true, __bf16>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
                        (const __bf16*)x, (const __bf16*)dy, (__bf16*)dx, h, w, c, ho, wo, relu_mask, accumulate, total);
