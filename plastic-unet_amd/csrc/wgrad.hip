@@ -1018,22 +1018,52 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
     }
 }
 
-// pass 2 with coalesced stores: block (c chunk of 64, row n) sums slab[.][n][tap*C + c] for its
-// 64 channels x taps (thread = (tap, c): 256-B coalesced reads per tap), transposes through LDS
-// and stores the contiguous [c][kh][kw] run of dweight[n] (the scatter above writes 4 B at a
-// 4*taps-byte stride).  Same fixed-order fp64 chains as wgrad_finish_kernel, so bit-identical.
-// bias_mode 0/1 (the ConvT bias, mode 2, stays on wgrad_finish_kernel).
+// pass 2 with coalesced stores: block (chunk of 256 channels, row n) sums slab[.][n][tap*C + c]
+// for its channels x taps (thread = (tap, 4 channels): 1-KB float4 reads per wave and split),
+// transposes through LDS and stores the contiguous [c][kh][kw] run of dweight[n] as float4 (the
+// scatter above writes 4 B at a 4*taps-byte stride).  Same fixed-order fp64 chains as
+// wgrad_finish_kernel, so bit-identical.  C % 4 == 0, 16-B aligned rows; bias_mode 0/1 (the ConvT
+// bias, mode 2, stays on wgrad_finish_kernel).
 template <typename T>
 __global__ __launch_bounds__(576) void wgrad_finish_t_kernel(const T* __restrict__ part, int G, int Nr, int Kc, int K,
                                                               int C, int taps, int bias_mode, float* __restrict__ dw,
                                                               float* __restrict__ db, int accumulate) {
-    __shared__ float tr[576];
+    __shared__ float tr[256 * 9];
+    typedef T t4 __attribute__((ext_vector_type(4)));
     const long long total = (long long)Nr * Kc;
     const int n = blockIdx.y;
-    const int c0 = blockIdx.x * 64;
-    const int tap = threadIdx.x >> 6, c = c0 + (threadIdx.x & 63);
-    auto sum = [&](long long idx) {
+    const int c0 = blockIdx.x * 256;
+    const int tap = threadIdx.x >> 6, cq = (threadIdx.x & 63) * 4;
+    const int cn = min(256, C - c0);
+    if (cq < cn) {
+        const long long idx = (long long)n * Kc + tap * C + c0 + cq;
+        double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0};
+        double s2[4] = {0.0, 0.0, 0.0, 0.0}, s3[4] = {0.0, 0.0, 0.0, 0.0};
+        int g = 0;
+        for (; g + 3 < G; g += 4) {
+            const t4 a = *reinterpret_cast<const t4*>(part + (long long)g * total + idx);
+            const t4 b = *reinterpret_cast<const t4*>(part + (long long)(g + 1) * total + idx);
+            const t4 c = *reinterpret_cast<const t4*>(part + (long long)(g + 2) * total + idx);
+            const t4 d = *reinterpret_cast<const t4*>(part + (long long)(g + 3) * total + idx);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                s0[e] += (double)a[e];
+                s1[e] += (double)b[e];
+                s2[e] += (double)c[e];
+                s3[e] += (double)d[e];
+            }
+        }
+        for (; g < G; ++g) {
+            const t4 a = *reinterpret_cast<const t4*>(part + (long long)g * total + idx);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s0[e] += (double)a[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tr[(cq + e) * taps + tap] = (float)((s0[e] + s1[e]) + (s2[e] + s3[e]));
+    }
+    if (bias_mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        const long long idx = (long long)n * Kc + K;
         int g = 0;
         for (; g + 3 < G; g += 4) {
             s0 += (double)part[(long long)g * total + idx];
@@ -1042,19 +1072,18 @@ __global__ __launch_bounds__(576) void wgrad_finish_t_kernel(const T* __restrict
             s3 += (double)part[(long long)(g + 3) * total + idx];
         }
         for (; g < G; ++g) s0 += (double)part[(long long)g * total + idx];
-        return (float)((s0 + s1) + (s2 + s3));
-    };
-    if (c < C) tr[(c - c0) * taps + tap] = sum((long long)n * Kc + tap * C + c);
-    if (bias_mode == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
-        const float v = sum((long long)n * Kc + K);
+        const float v = (float)((s0 + s1) + (s2 + s3));
         db[n] = accumulate ? db[n] + v : v;
     }
     __syncthreads();
-    const int cn = min(64, C - c0);
-    if ((int)threadIdx.x < cn * taps) {
-        float* o = dw + ((long long)n * C + c0) * taps + threadIdx.x;
-        const float v = tr[threadIdx.x];
-        *o = accumulate ? *o + v : v;
+    // dweight[n][c0 .. c0+cn)[taps] is cn * taps contiguous floats; 16-B aligned when C*taps and
+    // c0*taps are multiples of 4 (C % 4 == 0)
+    float* o = dw + ((long long)n * C + c0) * taps;
+    const int run = cn * taps;
+    for (int i = threadIdx.x * 4; i < run; i += blockDim.x * 4) {
+        f32x4 v = {tr[i], tr[i + 1], tr[i + 2], tr[i + 3]};
+        if (accumulate) v += *reinterpret_cast<const f32x4*>(o + i);
+        *reinterpret_cast<f32x4*>(o + i) = v;
     }
 }
 
@@ -1594,8 +1623,8 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
     const dim3 fgrid((unsigned)((threads + 255) / 256));
     const int taps = a->kh * a->kw;
-    if (a->bias_mode != 2 && taps <= 9) {
-        const dim3 tgrid((unsigned)ceil_div(pl.C, 64), (unsigned)a->n);
+    if (a->bias_mode != 2 && taps <= 9 && pl.C % 4 == 0 && pl.Kcp % 4 == 0 && ((uintptr_t)a->dweight & 15) == 0) {
+        const dim3 tgrid((unsigned)ceil_div(pl.C, 256), (unsigned)a->n);
         const dim3 tblock((unsigned)(64 * taps));
         if (pl.G == 1) {
             hipLaunchKernelGGL(wgrad_finish_t_kernel<float>, tgrid, tblock, 0, s, (const float*)workspace, pl.splits,
