@@ -1282,7 +1282,10 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
     const int N = a->n;
     const int T = a->k_pad / IG_BK;
     int target = 512;                 // ~2 resident blocks per CU (4-wave tiles)
-    if (N <= 64) {
+    if (N <= 32 && lean_ok(a)) {      // 32-channel layers (C4/C5 levels): no half-empty 64-wide tiles
+        *bn = 32;
+        *bm = blocks_for(M, N, 256, 32) >= 480 ? 256 : 128;
+    } else if (N <= 64) {
         *bn = 64;
         *bm = blocks_for(M, N, 256, 64) >= 480 ? 256 : 128;
     } else if (a->k_pad >= 2048) {
@@ -1444,6 +1447,8 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
             else if (bm == 256 && bn == 64) PU_XL(256, 64, 4, 1, 4);
             else if (bm == 128 && bn == 128) PU_XL(128, 128, 4, 1, 4);
             else if (bm == 128 && bn == 64) PU_XL(128, 64, 2, 2, 4);
+            else if (bm == 256 && bn == 32) PU_XL(256, 32, 4, 1, 4);
+            else if (bm == 128 && bn == 32) PU_XL(128, 32, 4, 1, 4);
             else done = false;
 #undef PU_XL
             if (done) {

@@ -29,6 +29,9 @@ LAYERS = {
     "l4_cat": (16, 512, 512, 256),
     "bottom": (8, 512, 0, 512),
     "stem": (128, 1, 0, 64),
+    # 32-channel levels of C4 (CoordConv base 8 at 64^2) / C5 (UNetpRes n8 at 128^2)
+    "c32": (64, 32, 0, 32),
+    "c32_cat": (64, 32, 32, 32),
     # small-channel direct-kernel levels of C4/C5 (UNetpRes neurons 8 at 512^2, CoordConv base 8)
     "s8": (512, 8, 0, 8),
     "s8_cat": (512, 8, 8, 8),
