@@ -154,18 +154,20 @@ __global__ void trace_kernel_v4(const float* __restrict__ H, const float* __rest
 
 
 // ------------------------------------------------------------------- fused head (outconv + head)
-// One block (1024 threads, one per CU) = 16 rows i0..i0+15 of slot b, all N columns.  Phases:
+// One block (512 threads, two per CU at N = 128) = 16 rows i0..i0+15 of slot b, all N columns.  Phases:
 //  1. outconv of the block's 16 rows and of row 0 (x0, needed by the trace update) into LDS:
 //     L lanes per pixel (L = C/4 up to 16), float4 channel loads, U pixels per lane group in
 //     flight, dot4_fma + xor-tree over the L lanes - the arithmetic of outconv_fwd_kernel (whose
 //     idle lanes add zeros), so X is bit-identical to the two-launch path;
 //  2. Weff_b = w + alpha (.) H_b in chunks of kc rows through LDS (all of it at N <= 128); Y = X Weff
-//     on v_mfma_f32_16x16x4_f32 (column tile t -> wave t mod 16) and y0 = x0 Weff as a VALU fmaf
+//     on v_mfma_f32_16x16x4_f32 (column tile t -> wave t mod 8) and y0 = x0 Weff as a VALU fmaf
 //     chain in the same k order (== the MFMA's, bitwise), so every block holds row 0's Y;
 //  3. Y = sigmoid, X rows written out (the backward's input);
 //  4. H'[k][j] for the block's rows k from H, x0[k], y0[j] (unet_p.py:81-86 operation order).
 constexpr int FH_R = 16;      // rows per block
-constexpr int FH_NT = 1024;   // threads per block
+constexpr int FH_NT = 512;    // threads per block (2 blocks per CU at nbf 128: one block's feature
+                               // loads overlap the other's GEMM / trace phases)
+constexpr int FH_WAVES = FH_NT / 64;
 constexpr int FH_LDS_W = 16384;   // floats of the Weff chunk (64 KB)
 
 template <typename T>
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
         __syncthreads();
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
-            const int tile = wave + 16 * t;
+            const int tile = wave + FH_WAVES * t;
             if (tile < tiles) {
                 const float* wcol = ws + (l >> 4) * N + tile * 16 + (l & 15);
                 const float* xrow = xs + (l & 15) * N + k0 + (l >> 4);
@@ -286,7 +288,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     // ---- 3. sigmoid + store (C layout of 16x16: column l & 15, rows 4 (l >> 4) + reg)
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-        const int tile = wave + 16 * t;
+        const int tile = wave + FH_WAVES * t;
         if (tile < tiles) {
             const int j = tile * 16 + (l & 15);
 #pragma unroll
@@ -581,7 +583,7 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
     const dim3 grid(N / FH_R, a->batch);
     const FastDiv dN = make_fastdiv(N);
     hipStream_t s = as_stream(stream);
-    const int tpw = (N / 16 + 15) / 16;                           // column tiles per wave (16 waves)
+    const int tpw = (N / 16 + FH_WAVES - 1) / FH_WAVES;           // column tiles per wave
 #define PU_FH2(T_, L_, W_)                                                                                     \
     hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat,     \
                        a->out_w, a->out_b, C, a->hebb, a->w, a->alpha, a->eta, a->x, a->y, a->hebb_out, N, dN, kc, \
@@ -589,7 +591,8 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
 #define PU_FH(T_, L_)                                                                                       \
     do {                                                                                                    \
         if (tpw <= 1) PU_FH2(T_, L_, 1);                                                                    \
-        else PU_FH2(T_, L_, 2);                                                                             \
+        else if (tpw <= 2) PU_FH2(T_, L_, 2);                                                               \
+        else PU_FH2(T_, L_, 4);                                                                             \
     } while (0)
 #define PU_FH_L(T_)                                                                                         \
     switch (L) {                                                                                            \
