@@ -1444,7 +1444,7 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         else hipLaunchKernelGGL((igemm_x6_lean_kernel<BM_, BN_, WM_, WN_, NW_, 1>), grid, dim3(NW_ * 64), 0, s, p); \
     } while (0)
             if (bm == 256 && bn == 128) PU_XL(256, 128, 8, 1, 8);
-            else if (bm == 256 && bn == 64) PU_XL(256, 64, 4, 1, 4);
+            else if (bm == 256 && bn == 64) PU_XL(256, 64, 8, 1, 8);   // 8 x 1 waves: fwd +3-4 % over 4 x 1
             else if (bm == 128 && bn == 128) PU_XL(128, 128, 4, 1, 4);
             else if (bm == 128 && bn == 64) PU_XL(128, 64, 2, 2, 4);
             else if (bm == 256 && bn == 32) PU_XL(256, 32, 4, 1, 4);

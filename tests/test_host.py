@@ -127,7 +127,7 @@ def test_pmc_kernel_tags_match_bench_tags():
     spec.loader.exec_module(m)
     assert m.tag_of("void pu::wgrad_halo_x6_kernel<2>(pu::WgradParams)") == "wgrad<128x576,halo,x6>"
     assert m.tag_of("void pu::wgrad_halo_x6_kernel<1>(pu::WgradParams)") == "wgrad<64x576,halo,x6>"
-    assert m.tag_of("void pu::igemm_x6_lean_kernel<256, 64, 4, 1, 4, 2>(pu::IgemmParams)") == "igemm<256x64,x6>"
+    assert m.tag_of("void pu::igemm_x6_lean_kernel<256, 64, 8, 1, 8, 2>(pu::IgemmParams)") == "igemm<256x64,x6>"
     assert m.tag_of("void pu::wgrad_dma_kernel<128, 256, 2, 2, 3, true, 4, true>(pu::WgradParams)") == \
         "wgrad<128x256,vec4,x6>"
     assert m.tag_of("pu::adam_kernel(pu::AdamBatch, float, float, float, float, float, float, float)") == "adam"
