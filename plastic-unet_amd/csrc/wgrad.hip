@@ -1160,6 +1160,7 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     int occ;  // resident blocks per CU (LDS / VGPR limited, from the resource-usage report)
     if (ext_k <= 64) { pl->BN = 64; pl->BK = 64; occ = pl->dma ? 6 : 7; }
     else if (ext_n <= 64 && !pl->dma) { pl->BN = 64; pl->BK = 256; occ = 3; }
+    else if (ext_n <= 32 && a->math == 1) { pl->BN = 32; pl->BK = 128; occ = 4; }   // 32-channel layers (C4/C5)
     else if (ext_n <= 64) {
         // BK 128 (4 resident blocks) unless 192 (3 resident) pads k less - e.g. K = 9 taps x 64
         const bool b192 = ceil_div(ext_k, 192) * 192 < ceil_div(ext_k, 128) * 128;
@@ -1794,6 +1795,7 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
         } else if (pl.dma) {
             if (pl.BK == 64) PU_WG_DMA(64, 64, 2, 2);
             else if (pl.BN == 64 && pl.BK == 128) PU_WG_DMA(64, 128, 2, 2);
+            else if (pl.BN == 32) PU_WG_DMA(32, 128, 1, 4);
             else if (pl.BK == 192) PU_WG_DMA(64, 192, 2, 2);
             else if (pl.BK == 256 && fq) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true, 4, true>), grid, dim3(256), 0, s, p);
             else if (pl.BK == 256) hipLaunchKernelGGL((wgrad_dma_kernel<128, 256, 2, 2, 3, true>), grid, dim3(256), 0, s, p);
