@@ -1141,6 +1141,39 @@ __global__ __launch_bounds__(256) void smallconv_kernel(const IgemmParams p) {
 }
 
 
+// 1x1 convolution with few channels (the CoordConv stem: AddCoords' 4 channels -> base_ch,
+// coord_conv_script.py:61-85): one thread per pixel, its C input channels as float4 loads, N
+// outputs as an fma chain over c in order (weights [n][k_pad] from the scalar cache), the shared
+// float4 epilogue.  HBM-bound: (C + N) * 4 bytes per pixel; the MFMA tile path pads K to 16 and
+// N to 64 (1/32 of the tile used).
+template <int C, int N>
+__global__ __launch_bounds__(256) void conv1x1_small_kernel(const IgemmParams p) {
+    for (long long m = blockIdx.x * 256LL + threadIdx.x; m < p.M; m += (long long)gridDim.x * 256) {
+        float x[C];
+#pragma unroll
+        for (int c = 0; c < C; c += 4) {
+            const f32x4 v = c < p.c0 ? *reinterpret_cast<const f32x4*>(p.src0 + m * p.c0 + c)
+                                     : *reinterpret_cast<const f32x4*>(p.src1 + m * p.c1 + (c - p.c0));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[c + e] = v[e];
+        }
+        const EpiRow er = epi_row(p, (int)m);
+#pragma unroll
+        for (int n = 0; n < N; n += 4) {
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float* w = p.wt + (n + e) * p.k_pad;
+                float acc = x[0] * w[0];
+#pragma unroll
+                for (int c = 1; c < C; ++c) acc = fmaf(x[c], w[c], acc);
+                v[e] = acc;
+            }
+            epi_store4(p, er, n, v);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- single-channel stem (C = 1)
 // The first 3x3 conv (inc.c0: 1 -> N channels, unet_p.py:208-215) is a K = 9 GEMM: nothing for
 // an MFMA tile to do, the layer is the write of its N-channel output.  A block stages the 1-channel
@@ -1316,6 +1349,14 @@ static void plan_tiles(const pu_conv_args* a, long long M, int* bm, int* bn, int
 
 // the small-channel direct convolution handles: 3x3 / s1 / p1 (same size), C in {1,4,8,12,16},
 // N in {4,8,16}, tap-major weight rows, float4 epilogue
+// the direct 1x1 kernel: k 1 / s1 / p0 (same size), C in {4, 8}, N in {8, 16}, plain float4 epilogue
+static bool conv1x1_small_ok(const pu_conv_args* a) {
+    const int C = a->c0 + a->c1;
+    return (C == 4 || C == 8) && (a->n == 8 || a->n == 16) && a->kh == 1 && a->kw == 1 && a->stride == 1 &&
+           a->pad == 0 && a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) &&
+           vec_epilogue(a) && a->c0 % 4 == 0 && a->c1 % 4 == 0 && (a->cgroup == 0 || a->cgroup >= C);
+}
+
 static bool small_conv_ok(const pu_conv_args* a) {
     const int C = a->c0 + a->c1;
     const bool cset = C == 1 || C == 4 || C == 8 || C == 12 || C == 16;
@@ -1413,6 +1454,15 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         else hipLaunchKernelGGL((stem_conv_kernel<32>), sgrid, dim3(256), 0, s, p);
         return check_launch("pu_conv_igemm (stem)");
     }
+    if (conv1x1_small_ok(a)) {
+        p.ksplit = 1;
+        const dim3 g1((unsigned)(M / 256 + 1 < 8192 ? M / 256 + 1 : 8192));
+        if (C == 4 && N == 8) hipLaunchKernelGGL((conv1x1_small_kernel<4, 8>), g1, dim3(256), 0, s, p);
+        else if (C == 4) hipLaunchKernelGGL((conv1x1_small_kernel<4, 16>), g1, dim3(256), 0, s, p);
+        else if (N == 8) hipLaunchKernelGGL((conv1x1_small_kernel<8, 8>), g1, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((conv1x1_small_kernel<8, 16>), g1, dim3(256), 0, s, p);
+        return check_launch("pu_conv_igemm (1x1 small-channel)");
+    }
     if (small_conv_ok(a)) {
         p.ksplit = 1;
         const dim3 sgrid((unsigned)(((a->out_w + SC_TW - 1) / SC_TW) * ((a->out_h + SC_TH - 1) / SC_TH) * a->batch));
@@ -1495,7 +1545,7 @@ extern "C" int pu_split_weight6(const float* packed, void* out, int n, int k_pad
 extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
     if (!a || a->batch <= 0 || a->out_h <= 0 || a->out_w <= 0 || a->n <= 0 || a->k_pad <= 0) return 0;
     const long long M = (long long)a->batch * a->out_h * a->out_w;
-    if (small_conv_ok(a) || stem_conv_ok(a)) return 0;
+    if (small_conv_ok(a) || stem_conv_ok(a) || conv1x1_small_ok(a)) return 0;
     int bm, bn, ks, tp;
     plan_tiles(a, M, &bm, &bn, &ks, &tp);
     return split_bytes(M, a->n, ks);
@@ -1512,6 +1562,13 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         *bm = ST_TH * ST_TW;
         *bn = a->n;
         *mode = 5;
+        if (ksplit) *ksplit = 1;
+        return PU_OK;
+    }
+    if (conv1x1_small_ok(a)) {       // reported as mode 3 ("direct"), one pixel per thread
+        *bm = 256;
+        *bn = a->n;
+        *mode = 3;
         if (ksplit) *ksplit = 1;
         return PU_OK;
     }

@@ -378,3 +378,25 @@ def test_pack_refresh_after_optimizer_is_one_launch():
         net(x, h)
     s = prof.summary()
     assert s["pack_weight"]["launches"] == 1, s.get("pack_weight")
+
+
+@pytest.mark.parametrize("C,N,relu", [(4, 8, True), (4, 16, False), (8, 8, True), (8, 16, True)])
+def test_conv1x1_small_channel(C, N, relu):
+    """the direct 1x1 kernel (CoordConv stem, coord_conv_script.py:61-85) vs CPU fp32"""
+    from punet._lib import PU_PACK_CONV_FWD
+    g = torch.Generator().manual_seed(C * 10 + N)
+    B, H, W = 2, 33, 40
+    x = rnd(B, C, H, W, g=g)
+    w = rnd(N, C, 1, 1, g=g, scale=0.5)
+    b = rnd(N, g=g)
+    ref = F.conv2d(x, w, b)
+    if relu:
+        ref = torch.relu(ref)
+    pk = T._Packs()
+    xd = nhwc(x).to(DEV)
+    y = torch.empty(B, H, W, N, device=DEV)
+    wd = w.to(DEV)
+    K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, src0=xd, c0=C,
+            weight=pk.get(wd, PU_PACK_CONV_FWD, K.round16(C)), k_pad=K.round16(C), n=N, bias=b.to(DEV),
+            dst0=y, relu=relu)
+    assert_close(nchw(y), ref)
