@@ -520,6 +520,19 @@ __global__ void channel_scale_kernel(const float* __restrict__ x, const float* _
 // AddCoords + NCHW->NHWC: one thread per output element (channel fastest); fp32 with no
 // contraction so the coordinate values are those of the elementwise CPU ops
 #pragma clang fp contract(off)
+// c == 1 with r (the CoordConv U-Net's input): one thread per pixel, one float4 store
+// {x, xx, yy, r}; the same float expressions as add_coords_kernel (bit-identical), 32-bit index math
+__global__ void add_coords4_kernel(const float* __restrict__ x, float* __restrict__ out, int h, int w, int pixels) {
+    for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < pixels; pix += gridDim.x * blockDim.x) {
+        const int rem = pix % (h * w);
+        const int i = rem / w, j = rem - i * w;
+        const float xx = ((float)j / (float)(h - 1)) * 2.0f - 1.0f;
+        const float yy = ((float)i / (float)(w - 1)) * 2.0f - 1.0f;
+        const float dx = xx - 0.5f, dy = yy - 0.5f;
+        *reinterpret_cast<f32x4*>(out + 4LL * pix) = f32x4{x[pix], xx, yy, sqrtf(dx * dx + dy * dy)};
+    }
+}
+
 __global__ void add_coords_kernel(const float* __restrict__ x, float* __restrict__ out, int c, int h, int w,
                                   int with_r, long long total) {
     const int co = c + 2 + with_r;
@@ -857,7 +870,13 @@ extern "C" int pu_column_sum(const float* x, long long rows, int cols, float* ou
 extern "C" int pu_add_coords(const float* x, float* out, int batch, int c, int h, int w, int with_r, void* stream) {
     PU_REQUIRE(x && out && batch > 0 && c > 0 && h > 1 && w > 1 && (with_r == 0 || with_r == 1),
                "pu_add_coords: bad args");
-    const long long total = (long long)batch * h * w * (c + 2 + with_r);
+    const long long pixels = (long long)batch * h * w;
+    if (c == 1 && with_r && ((uintptr_t)out & 15) == 0 && pixels < (1LL << 31)) {
+        hipLaunchKernelGGL(add_coords4_kernel, dim3(grid_for(pixels)), dim3(256), 0, as_stream(stream), x, out, h, w,
+                           (int)pixels);
+        return check_launch("pu_add_coords");
+    }
+    const long long total = pixels * (c + 2 + with_r);
     hipLaunchKernelGGL(add_coords_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, out, c, h, w,
                        with_r, total);
     return check_launch("pu_add_coords");
