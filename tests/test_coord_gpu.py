@@ -16,14 +16,15 @@ import oracle  # noqa: E402
 DEV = torch.device("cuda")
 
 
-@pytest.mark.parametrize("with_r", [False, True])
-def test_add_coords_kernel(with_r):
+@pytest.mark.parametrize("with_r,c,w", [(False, 3, 17), (True, 3, 17), (True, 1, 19), (False, 1, 19)])
+def test_add_coords_kernel(with_r, c, w):
+    """c = 1 with r takes the one-float4-per-pixel kernel (the CoordConv U-Net's input)"""
     g = torch.Generator().manual_seed(1)
-    x = torch.rand(2, 3, 17, 17, generator=g)
+    x = torch.rand(2, c, 17, w, generator=g)
     got = K.add_coords(x.to(DEV), with_r).cpu()
     ref = oracle.add_coords(x, with_r=with_r).permute(0, 2, 3, 1)
     torch.testing.assert_close(got, ref, rtol=0, atol=2e-7)
-    assert torch.equal(got[..., :3], ref[..., :3])
+    assert torch.equal(got[..., :c + 2], ref[..., :c + 2])
 
 
 @pytest.mark.parametrize("with_r,depth,base", [(True, 4, 8), (False, 3, 16)])
