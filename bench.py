@@ -4,6 +4,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher (no WORLD_SIZE in the environment), --gpus N > 1 makes this process spawn N
+rank processes itself (launch_workers: torchrun's env, MASTER_ADDR 127.0.0.1, a free port) and
+exit with their status.  Every rank checks after init_process_group("nccl") that the world has
+exactly N ranks and that N GPUs are visible, and exits non-zero otherwise.
+
 Workload = config C2 (BASELINE.json configs[1]): UNetp depth 5 / base 64 (14.81 M params), Oja
 rule, 1x128x128 synthetic tiles, batch 32 per GPU, fp32.  --config c4 / c5 measure the other
 single-GPU configurations (CoordConv U-Net 256x256 bs 32; UNetpRes neurons 8 512x512 bs 16 per GPU
@@ -191,12 +196,68 @@ def oja_update_bench(K, B, N, device, feat_channels=64):
     return res
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_workers(n, argv, cmd=None, poll_s=0.2):
+    """`python bench.py --gpus N` without a launcher: start N worker processes (one per GPU) with
+    torchrun's environment (WORLD_SIZE, RANK, LOCAL_RANK, MASTER_ADDR=127.0.0.1, MASTER_PORT) and
+    wait for them.  Runs before anything touches the GPU (the parent never initialises HIP; the
+    workers are fresh processes, not an exec).  If a worker fails the others are terminated (by
+    their own PIDs).  Returns rank 0's exit code, or the first non-zero one."""
+    import subprocess
+    port = _free_port()
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"WORLD_SIZE": str(n), "RANK": str(r), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "PU_BENCH_WORKER": "1"})
+        procs.append(subprocess.Popen(cmd + list(argv), env=env))
+    rcs = [None] * n
+    failed = None
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0) and failed is None:
+                    failed = r
+                    print("bench: rank %d exited with %d; stopping the other ranks" % (r, rcs[r]), file=sys.stderr)
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+        time.sleep(poll_s)
+    return rcs[failed] if failed is not None else rcs[0]
+
+
+def check_world(expected, world, devices=None):
+    """Exit non-zero when the process group does not have the --gpus ranks asked for, or when
+    fewer GPUs are visible than ranks (each rank needs its own device)."""
+    if world != expected:
+        print("bench: --gpus %d but the process group has %d ranks" % (expected, world), file=sys.stderr)
+        sys.exit(3)
+    if devices is not None and devices < expected:
+        print("bench: --gpus %d but only %d GPU(s) visible" % (expected, devices), file=sys.stderr)
+        sys.exit(3)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # torch.cuda.device_count() does not initialise the GPU on this image: safe before spawning
+        check_world(args.gpus, args.gpus, torch.cuda.device_count())
+        sys.exit(launch_workers(args.gpus, sys.argv[1:]))
     from punet import dp
     world, rank, local = dp.init_from_env("nccl")
-    if world != args.gpus and rank == 0:
-        print("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
+    if dist.is_initialized():
+        world = dist.get_world_size()
+    check_world(args.gpus, world, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
 
@@ -235,10 +296,13 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    per_rank = [elapsed]
     if world > 1:
         t = torch.tensor([elapsed], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        ts_all = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(ts_all, t)
+        per_rank = [x.item() for x in ts_all]
+        elapsed = max(per_rank)
     final_loss = loss.item() if loss is not None else float("nan")
 
     # ---------------- instrumented pass: per-launch HIP events on the launching stream
@@ -323,6 +387,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "world_size_seen": world,
+            "per_rank_ms_per_step": [round(e * 1e3 / args.steps, 3) for e in per_rank],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

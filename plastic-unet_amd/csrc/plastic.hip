@@ -170,6 +170,17 @@ constexpr int FH_NT = 512;    // threads per block (2 blocks per CU at nbf 128: 
 constexpr int FH_WAVES = FH_NT / 64;
 constexpr int FH_LDS_W = 16384;   // floats of the Weff chunk (64 KB)
 
+// Weff rows per LDS chunk: all N rows when N x N fits, else the largest multiple of 4 (the MFMA's
+// k step) that divides N and fits (N % 16 == 0, so 16 always qualifies: N = 144 -> 72, 192 -> 64,
+// 320 -> 40, 384 -> 32, 512 -> 32).  The chunk loop steps k0 by kc up to N, so kc must divide N.
+inline int fused_head_chunk(int N) {
+    if (N * N <= FH_LDS_W) return N;
+    int best = 16;
+    for (int d = 4; d * N <= FH_LDS_W && d <= N; d += 4)
+        if (N % d == 0) best = d;
+    return best;
+}
+
 template <typename T>
 __device__ __forceinline__ f32x4 fh_ld4(const T* p);
 template <>
@@ -181,7 +192,7 @@ __device__ __forceinline__ f32x4 fh_ld4<__bf16>(const __bf16* p) {
     return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
 
-template <typename T, int L, int TPW>
+template <typename T, int L, int TPW, bool PIPE>
 __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ wo,
                                                                const float* __restrict__ bo, int C,
                                                                const float* __restrict__ H, const float* __restrict__ w,
@@ -202,7 +213,77 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     const float* Hb = H + (long long)b * nn;
 
     // ---- 1. outconv
-    {
+    if constexpr (PIPE) {
+        // C == 4 L (one float4 per lane and pixel) and all of Weff in one LDS chunk: the feature
+        // loads of pass p + 1 are in flight while pass p is reduced (two register sets), and one
+        // float4 of w / alpha / H (Weff piece p) rides along with every pass, so the Weff build
+        // costs no round trips of its own.  Same arithmetic as the loop below (bit-identical).
+        constexpr int U = L >= 8 ? 8 : 4;
+        constexpr int PPP = FH_NT / L;
+        constexpr int PER = U * PPP;
+        const float bias = bo ? bo[0] : 0.f;
+        const int lane = tid % L;
+        const int npix = (fuse ? FH_R + 1 : FH_R) * N;
+        const int npass = (npix + PER - 1) / PER;
+        const int nw4 = N * N / 4;
+        const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + lane * 4);
+        f32x4 va[U], vb[U];
+        f32x4 pw, pa, ph;
+        auto load = [&](f32x4 (&v)[U], int p) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int q = min(p * PER + tid / L + u * PPP, npix - 1);
+                const int r = (int)fdiv((unsigned)q, dN), k = q - r * N;
+                v[u] = fh_ld4<T>(fb + ((long long)(r < FH_R ? i0 + r : 0) * N + k) * C + lane * 4);
+            }
+        };
+        auto load_piece = [&](int p) {
+            const int e4 = min(p * FH_NT + tid, nw4 - 1);
+            pw = reinterpret_cast<const f32x4*>(w)[e4];
+            pa = reinterpret_cast<const f32x4*>(alpha)[e4];
+            ph = reinterpret_cast<const f32x4*>(Hb)[e4];
+        };
+        auto store_piece = [&](int p) {
+#pragma clang fp contract(off)
+            const int e4 = p * FH_NT + tid;
+            if (e4 < nw4) {
+                f32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = pw[e] + pa[e] * ph[e];     // torch: w + mul(alpha, hebb)
+                reinterpret_cast<f32x4*>(ws)[e4] = o;
+            }
+        };
+        auto reduce = [&](f32x4 (&v)[U], int p) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float t = 0.f;
+                t += dot4_fma(v[u], ww);
+                if (L >= 16) t += __shfl_xor(t, 8, 16);
+                if (L >= 8) t += __shfl_xor(t, 4, 16);
+                if (L >= 4) t += __shfl_xor(t, 2, 16);
+                if (L >= 2) t += __shfl_xor(t, 1, 16);
+                const int q = p * PER + tid / L + u * PPP;
+                if (lane == 0 && q < npix) xs[q] = t + bias;
+            }
+        };
+        load(va, 0);
+        for (int p = 0; p < npass; p += 2) {
+            if (p + 1 < npass) load(vb, p + 1);
+            load_piece(p);
+            reduce(va, p);
+            store_piece(p);
+            if (p + 1 < npass) {
+                if (p + 2 < npass) load(va, p + 2);
+                load_piece(p + 1);
+                reduce(vb, p + 1);
+                store_piece(p + 1);
+            }
+        }
+        for (int p = npass; p * FH_NT < nw4; ++p) {
+            load_piece(p);
+            store_piece(p);
+        }
+    } else {
         constexpr int U = L >= 8 ? 8 : 4;       // pixels per lane group in flight
         const float bias = bo ? bo[0] : 0.f;
         const int lane = tid % L;
@@ -243,6 +324,11 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     // X rows of this block -> global (coalesced)
     for (int e = tid; e < FH_R * N; e += FH_NT) X[(long long)b * nn + (long long)i0 * N + e] = xs[e];
 
+    // the trace update's first float4 of H (rows i0.., L2-resident after the Weff build), in
+    // flight during the GEMM
+    f32x4 hpre = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (fuse && tid < FH_R * N / 4) hpre = reinterpret_cast<const f32x4*>(Hb + (long long)i0 * N)[tid];
+
     // ---- 2. GEMM
     const int wave = tid >> 6, l = tid & 63;
     const int tiles = N / 16;
@@ -251,7 +337,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float acc0 = 0.f;                                  // y0 chain of column tid (tid < N)
     for (int k0 = 0; k0 < N; k0 += kc) {
-        {
+        if (!PIPE) {
 #pragma clang fp contract(off)
             const int ne = kc * N;
             for (int e0 = tid; e0 < ne; e0 += 8 * FH_NT) {
@@ -305,11 +391,17 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     // ---- 4. trace update of rows k = i0 .. i0+15
     const float eta = eta_p[0];
     const float one_m_eta = 1.f - eta;
-    float* Hnb = Hn + (long long)b * nn;
-    for (int e = tid; e < FH_R * N; e += FH_NT) {
-        const int kk = (int)fdiv((unsigned)e, dN), j = e - kk * N;
-        const long long o = (long long)(i0 + kk) * N + j;
-        Hnb[o] = trace_rule(Hb[o], xs[FH_R * N + i0 + kk], y0s[j], eta, one_m_eta, rule);
+    // rows i0 .. i0+15 of H / H' are contiguous: float4 over the block's FH_R * N elements
+    const f32x4* Hr = reinterpret_cast<const f32x4*>(Hb + (long long)i0 * N);
+    f32x4* Hnr = reinterpret_cast<f32x4*>(Hn + (long long)b * nn + (long long)i0 * N);
+    for (int e4 = tid; e4 < FH_R * N / 4; e4 += FH_NT) {
+        const f32x4 h = e4 == tid ? hpre : Hr[e4];
+        const int kk = (int)fdiv((unsigned)(4 * e4), dN), j = 4 * e4 - kk * N;
+        const float x0 = xs[FH_R * N + i0 + kk];
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = trace_rule(h[e], x0, y0s[j + e], eta, one_m_eta, rule);
+        Hnr[e4] = o;
     }
 }
 
@@ -576,18 +668,26 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
     PU_REQUIRE(a->rule == PU_RULE_HEBB || a->rule == PU_RULE_OJA, "Must select one learning rule ('hebb' or 'oja')");
     PU_REQUIRE(!a->hebb_out || (a->eta && a->hebb_out != a->hebb), "pu_plastic_head_fwd: hebb_out needs eta and no aliasing");
     PU_REQUIRE((long long)N * N * C * a->batch < (1LL << 40), "pu_plastic_head_fwd: too large");
+    PU_REQUIRE((((uintptr_t)a->hebb | (uintptr_t)a->w | (uintptr_t)a->alpha | (uintptr_t)a->hebb_out) & 15) == 0,
+               "pu_plastic_head_fwd: hebb / w / alpha / hebb_out must be 16-byte aligned");
     const int q = C / 4;
     const int L = q >= 16 ? 16 : (q & (q - 1)) == 0 ? q : 16;    // lanes per pixel
-    const int kc = N * N <= FH_LDS_W ? N : FH_LDS_W / N;          // Weff rows per LDS chunk
+    const int kc = fused_head_chunk(N);                           // Weff rows per LDS chunk
+    const bool pipe = C == 4 * L && kc == N;
     const size_t lds = ((size_t)(FH_R + 1) * N + (size_t)kc * N + N) * sizeof(float);
     const dim3 grid(N / FH_R, a->batch);
     const FastDiv dN = make_fastdiv(N);
     hipStream_t s = as_stream(stream);
     const int tpw = (N / 16 + FH_WAVES - 1) / FH_WAVES;           // column tiles per wave
-#define PU_FH2(T_, L_, W_)                                                                                     \
-    hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat,     \
+#define PU_FH3(T_, L_, W_, P_)                                                                                     \
+    hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_, P_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat,     \
                        a->out_w, a->out_b, C, a->hebb, a->w, a->alpha, a->eta, a->x, a->y, a->hebb_out, N, dN, kc, \
                        a->rule)
+#define PU_FH2(T_, L_, W_)                                                                                     \
+    do {                                                                                                       \
+        if (pipe) PU_FH3(T_, L_, W_, true);                                                                    \
+        else PU_FH3(T_, L_, W_, false);                                                                        \
+    } while (0)
 #define PU_FH(T_, L_)                                                                                       \
     do {                                                                                                    \
         if (tpw <= 1) PU_FH2(T_, L_, 1);                                                                    \
@@ -606,6 +706,7 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
 #undef PU_FH_L
 #undef PU_FH
 #undef PU_FH2
+#undef PU_FH3
     return check_launch("pu_plastic_head_fwd");
 }
 

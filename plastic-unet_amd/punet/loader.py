@@ -75,6 +75,13 @@ class BatchPrefetcher:
     def __iter__(self):
         if not self.ranges:
             return
+        if self.gpu:
+            # a caller that stops iterating early (zip over the ranges ends before the generator
+            # resumes past its last yield) never recorded the last slot's consumed event: order
+            # every slot's next copy after all the compute work enqueued so far
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.consumed = [ev] * self.depth
         for j in range(min(self.depth - 1, len(self.ranges))):
             self._fill(j)
         for i, (lo, hi) in enumerate(self.ranges):

@@ -27,7 +27,7 @@ import torch
 
 from . import kernels as K
 from ._lib import PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_DGRAD, PU_PACK_CONVT3_FWD
-from .trunk import _Packs
+from .trunk import _Packs, _grad_sinks
 
 
 # ------------------------------------------------------------------------------ layer helpers
@@ -202,10 +202,7 @@ class ResTrunk:
             gb.ready(*self.params[i:i + n])
 
     def grad_sinks(self):
-        gb = self.gradbuf
-        if gb is None or any(p.grad is not None for p in self.params):
-            return None
-        return [gb.view_for(p) for p in self.params]
+        return _grad_sinks(self, self.slots["outc"])
 
     def _mask(self, name, B, C, p, device):
         if self.mask_fn is not None:

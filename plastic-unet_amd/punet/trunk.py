@@ -55,6 +55,20 @@ class _Packs:
                 self.cache[key] = (w._version, packed, w)
 
 
+def _grad_sinks(trunk, outc):
+    """Views of trunk.gradbuf for trunk.params, or None when a parameter already holds a .grad
+    (the backward would then accumulate into an aliased buffer).  With trunk.fused_head the
+    outconv weight/bias (params[outc], params[outc+1]) belong to the head: its backward runs first
+    and autograd has already adopted their views, so they are not checked."""
+    gb = trunk.gradbuf
+    if gb is None:
+        return None
+    skip = (outc, outc + 1) if trunk.fused_head else ()
+    if any(p.grad is not None for i, p in enumerate(trunk.params) if i not in skip):
+        return None
+    return [gb.view_for(p) for p in trunk.params]
+
+
 def _kp(k, dt):
     """K padded to the kernel's stage: 16 fp32 or 32 bf16 values."""
     return K.round16(k) if dt == torch.float32 else (k + 31) // 32 * 32
@@ -266,11 +280,9 @@ class UNetpTrunk:
     def grad_sinks(self):
         """Views of the flat gradient buffer to write into, or None.  Only used when every
         parameter's .grad is None (autograd then adopts the views; if a .grad already existed it
-        would accumulate into an aliased buffer)."""
-        gb = self.gradbuf
-        if gb is None or any(p.grad is not None for p in self.params):
-            return None
-        return [gb.view_for(p) for p in self.params]
+        would accumulate into an aliased buffer).  With the fused head the outconv parameters
+        are the head's (its backward runs first and writes their views), so they do not count."""
+        return _grad_sinks(self, self.slot["outc"])
 
     # -------------------------------------------------------------------------------- forward
     def _conv(self, key, P, s, x0, x1=None):

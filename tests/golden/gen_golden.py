@@ -24,6 +24,8 @@ Fixtures (each < 2 MB):
   unetp_{bn,bilinear,bn_bilinear}.npz  UNetp(batch_norm / bilinear_upsample) at 64x64: init, two
                                  train-mode forwards (running statistics), grads, eval forward
   unetpres_bn.npz                UNetpRes(neurons=4, batch_norm=True, dropout 0) at 64x64, the same
+  tgs_split.npz                  reference load_train_dataset (data_set.py:18-63) on a synthetic TGS
+                                 directory (tests/tgs_fixture.py): the stratified split, 24^2 and 32^2
 """
 import os
 import sys
@@ -490,6 +492,40 @@ def gen_iou_batch():
     thresholds = np.log(np.linspace(0.3, 0.7, 31) / (1 - np.linspace(0.3, 0.7, 31)))
     ious = np.array([mod.iou_metric_batch(y_valid, preds > th) for th in thresholds])
     save("iou_batch.npz", y_valid=y_valid, preds=preds, thresholds=thresholds, ious=ious)
+
+
+def gen_tgs_split():
+    """The reference's load_train_dataset (src/utils/data_set.py:18-63: CSV join, masks / 65535,
+    coverage classes, stratified train_test_split(random_state=42)) on a synthetic TGS directory,
+    at the source size (no resize) and resized 24 -> 32.  Its ``from utils import load_image``
+    is satisfied by the BUILD's own load_image (skimage is absent), so the fixture pins the split,
+    the class logic and the array layout, not the resize."""
+    import importlib.util
+    sys.path.insert(0, os.path.join(os.path.dirname(OUT), "..", "plastic-unet_amd"))
+    from utils import data_set as build_ds          # noqa: E402  (the build's utils package)
+    saved = {k: sys.modules.pop(k) for k in list(sys.modules) if k == "utils" or k.startswith("utils.")}
+    stub = types.ModuleType("utils")
+    stub.load_image = build_ds.load_image
+    stub.plot_coverage = stub.plot_depth = lambda *a, **k: None
+    sys.modules["utils"] = stub
+    try:
+        spec = importlib.util.spec_from_file_location("ref_data_set", os.path.join(REF, "utils/data_set.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        sys.path.insert(0, os.path.dirname(OUT))
+        from tgs_fixture import tgs_synthetic_inputs, write_tgs_dir   # noqa: E402  (tests/tgs_fixture.py)
+        arrs = tgs_synthetic_inputs()
+        out = dict(arrs)
+        with tempfile.TemporaryDirectory() as d:
+            write_tgs_dir(d, arrs)
+            for tag, S in (("s24", 24), ("s32", 32)):
+                xt, xv, yt, yv = mod.load_train_dataset(d, S, S, 1, val_ratio=0.2)
+                out.update({tag + "_x_train": xt, tag + "_x_valid": xv, tag + "_y_train": yt, tag + "_y_valid": yv})
+    finally:
+        for k in [k for k in sys.modules if k == "utils" or k.startswith("utils.")]:
+            del sys.modules[k]
+        sys.modules.update(saved)
+    save("tgs_split.npz", **out)
 
 
 if __name__ == "__main__":

@@ -41,9 +41,10 @@ def _run(net_ctor, lo, hi, dev, bucket_mb):
     tr = Trainer(net, lr=1e-3, steplr=1e5, bucket_mb=bucket_mb)
     xs, ts = _data()
     hebb = net.initialZeroHebb(hi - lo)
-    out = {"loss": [], "grads": [], "overlapped": []}
+    out = {"loss": [], "grads": [], "overlapped": [], "owns": []}
     for s in range(STEPS):
         loss, hebb = tr.step(xs[s][lo:hi].to(dev), ts[s][lo:hi].to(dev), hebb)
+        out["owns"].append(tr.gradbuf.owns_grads())     # every grad landed in the flat buffer
         if dist.is_initialized():
             dist.all_reduce(loss, op=dist.ReduceOp.SUM)
             loss /= dist.get_world_size()
@@ -83,7 +84,9 @@ def test_overlapped_dp_matches_single_process(tmp_path, gpu_device):
     ref = _run(_ctor, 0, B, gpu_device, bucket_mb=16)
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     res = [torch.load(os.path.join(tmp_path, "r%d.pt" % r), weights_only=True) for r in range(world)]
+    assert all(ref["owns"])
     for r in res:
+        assert all(r["owns"]), r["owns"]       # the fused head's outconv grads do not divert the trunk's
         assert all(o >= 2 for o in r["overlapped"]), r["overlapped"]    # buckets went out during backward
         for s in range(STEPS):
             assert abs(r["loss"][s] - ref["loss"][s]) < 1e-5 * abs(ref["loss"][s])
@@ -111,9 +114,10 @@ def _worker_nccl(rank, world, port, out_dir):
     assert tr.reducer is not None
     xs, ts = _data()
     hebb = net.initialZeroHebb(B)
-    out = {"loss": [], "grads": [], "overlapped": []}
+    out = {"loss": [], "grads": [], "overlapped": [], "owns": []}
     for s in range(STEPS):
         loss, hebb = tr.step(xs[s].to(dev), ts[s].to(dev), hebb)
+        out["owns"].append(tr.gradbuf.owns_grads())
         out["loss"].append(loss.item())
         out["grads"].append({n: p.grad.detach().cpu().clone() for n, p in net.named_parameters()
                              if p.grad is not None})
@@ -143,6 +147,7 @@ def test_rccl_async_bucket_path_world1(tmp_path, gpu_device):
     ref_params = {n: p.detach().cpu().clone() for n, p in net.named_parameters()}
     mp.spawn(_worker_nccl, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
     r = torch.load(os.path.join(tmp_path, "nccl.pt"), weights_only=True)
+    assert all(r["owns"]), r["owns"]
     assert all(o >= 2 for o in r["overlapped"]), r["overlapped"]
     assert r["loss"] == ref_loss
     for s in range(STEPS):

@@ -1,5 +1,6 @@
 """Host-side logic on CPU: the build's IoU metric / RLE match the reference fixtures, batching of
 the training loop, CLI parsing."""
+import os
 import numpy as np
 
 from conftest import golden
@@ -131,3 +132,25 @@ def test_pmc_kernel_tags_match_bench_tags():
     assert m.tag_of("void pu::wgrad_dma_kernel<128, 256, 2, 2, 3, true, 4, true>(pu::WgradParams)") == \
         "wgrad<128x256,vec4,x6>"
     assert m.tag_of("pu::adam_kernel(pu::AdamBatch, float, float, float, float, float, float, float)") == "adam"
+
+
+def test_tgs_split_matches_reference_load_train_dataset(tmp_path):
+    """The build's load_train_dataset (utils/data_set.py) against the reference's own
+    (src/utils/data_set.py:18-63, run by tests/golden/gen_golden.py gen_tgs_split on the same
+    synthetic directory): identical train/valid arrays in identical order, without and with the
+    24 -> 32 resize.  Pins the CSV join, masks / 65535, coverage classes and the stratified
+    random_state=42 split; the resize itself is the build's on both sides (skimage absent)."""
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from tgs_fixture import write_tgs_dir
+    from utils.data_set import load_train_dataset
+    ref = golden("tgs_split.npz")
+    write_tgs_dir(str(tmp_path), ref)
+    for tag, S in (("s24", 24), ("s32", 32)):
+        got = load_train_dataset(str(tmp_path), S, S, 1, val_ratio=0.2)
+        for name, arr in zip(("x_train", "x_valid", "y_train", "y_valid"), got):
+            exp = ref[tag + "_" + name]
+            assert arr.shape == exp.shape and arr.dtype == exp.dtype, (tag, name, arr.shape, exp.shape)
+            assert np.array_equal(arr, exp), (tag, name)
+    assert ref["s24_x_valid"].shape[0] == 8            # 20 % of 40, 5 coverage classes x 8

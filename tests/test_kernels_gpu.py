@@ -310,7 +310,13 @@ def test_fused_head_trace_equals_two_launch_path(B, N, rule):
 @pytest.mark.parametrize("rule", [0, 1])
 @pytest.mark.parametrize("B,N,C,dt", [(3, 128, 64, torch.float32), (2, 32, 8, torch.float32),
                                       (2, 64, 12, torch.float32), (1, 512, 8, torch.float32),
-                                      (2, 48, 128, torch.float32), (3, 128, 64, torch.bfloat16)])
+                                      (2, 48, 128, torch.float32), (3, 128, 64, torch.bfloat16),
+                                      # N > 128 whose Weff does not fit one LDS chunk and is not a
+                                      # power of two (chunk 72 / 64 / 40 / 32 rows)
+                                      (2, 144, 64, torch.float32), (1, 192, 16, torch.float32),
+                                      (1, 320, 8, torch.float32), (1, 384, 64, torch.float32),
+                                      # the pipelined single-chunk path (C == 4 L) at every L
+                                      (4, 64, 4, torch.float32), (2, 112, 32, torch.bfloat16)])
 def test_fused_head_equals_outconv_then_head(rule, B, N, C, dt):
     """pu_plastic_head_fwd (outconv + Weff GEMM on v_mfma_f32_16x16x4_f32 + sigmoid + trace update,
     one launch) is bit-identical to the two-kernel path outconv_fwd -> plastic_fwd: the outconv sum
