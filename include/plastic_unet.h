@@ -95,7 +95,10 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
 /* PU_CONV_NO_HALO: a dispatch hint, not an epilogue flag - keep a bf16 3x3/s1 layer that the halo
  * kernel would take (width 32/64/128) on the per-tap lean kernel (A/B runs and the bit-identity
  * test: both compute the same sums in the same order when the per-tap launch is not split) */
-enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8, PU_CONV_NO_HALO = 16 };
+/* PU_CONV_HALO_V1: a dispatch hint - take the register-staged 256-pixel halo kernel instead of the
+ * DMA-ring 512-pixel one (A/B runs; the per-tap bit-identity test) */
+enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8, PU_CONV_NO_HALO = 16,
+       PU_CONV_HALO_V1 = 32 };
 
 typedef struct {
     int batch;

@@ -1067,19 +1067,30 @@ __global__ __launch_bounds__(256) void smallconv_kernel(const IgemmParams p) {
 
     // stage the halo: element (hy, hx, c) from src0 (c < c0) or src1
     if (C % 4 == 0 && p.c0 % 4 == 0) {
-        constexpr int Q = C / 4;
-        for (int e = threadIdx.x; e < HH * HWD * Q; e += 256) {
+        // every float4 of the halo a thread stages is loaded before any is stored (one round trip
+        // per block instead of one per float4: 5 for C = 8, 10 for C = 16)
+        constexpr int Q = C / 4 > 0 ? C / 4 : 1;     // (C == 1 never takes this branch)
+        constexpr int NE = HH * HWD * Q;
+        constexpr int PT = (NE + 255) / 256;
+        f32x4 v[PT];
+#pragma unroll
+        for (int it = 0; it < PT; ++it) {
+            const int e = it * 256 + threadIdx.x;
             const int q = e % Q, pix = e / Q;
             const int hx = pix % HWD, hy = pix / HWD;
             const int gy = y0 + hy, gx = x0 + hx;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
+            v[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (e < NE && (unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
                 const long long px = img + (long long)gy * p.Wi + gx;
                 const int c = 4 * q;
-                v = c < p.c0 ? *reinterpret_cast<const f32x4*>(p.src0 + px * p.c0 + c)
-                             : *reinterpret_cast<const f32x4*>(p.src1 + px * p.c1 + (c - p.c0));
+                v[it] = c < p.c0 ? *reinterpret_cast<const f32x4*>(p.src0 + px * p.c0 + c)
+                                 : *reinterpret_cast<const f32x4*>(p.src1 + px * p.c1 + (c - p.c0));
             }
-            *reinterpret_cast<f32x4*>(tile + pix * CP + 4 * q) = v;
+        }
+#pragma unroll
+        for (int it = 0; it < PT; ++it) {
+            const int e = it * 256 + threadIdx.x;
+            if (e < NE) *reinterpret_cast<f32x4*>(tile + (e / Q) * CP + 4 * (e % Q)) = v[it];
         }
     } else {
         for (int e = threadIdx.x; e < HH * HWD * CP; e += 256) {

@@ -101,6 +101,75 @@ __device__ __forceinline__ void epi_store4_b(const IgemmBf16Params& p, const Epi
     *reinterpret_cast<bf16x4*>(dst + off) = o;
 }
 
+// the same epilogue for channels n..n+7 of pixel m (non-SHUFFLE2, n0 % 8 == 0): 16-byte loads and
+// stores, so 8 lanes cover a 64-channel pixel row of 128 contiguous bytes.  bias: preloaded.
+// Every lane issues the same memory operations (a lane whose destination has no mask still loads,
+// from a valid address, and ignores it), so the caller can count them for s_waitcnt: 1 store +
+// one load each for resid / mask / accumulate when the launch uses them (epi8_ops).
+__device__ __forceinline__ int epi8_ops(const IgemmBf16Params& p) {
+    return 1 + (p.resid ? 1 : 0) + ((p.mask0 || p.mask1) ? 1 : 0) + ((p.flags & PU_EPI_ACCUM) ? 1 : 0);
+}
+
+__device__ __forceinline__ void epi_store8_b(const IgemmBf16Params& p, long long m, int n, f32x4 v0, f32x4 v1,
+                                             f32x4 b0, f32x4 b1) {
+    __bf16* dst;
+    const __bf16* msk;
+    long long off;
+    if (n < p.n0) {
+        off = m * p.n0 + n;
+        dst = p.dst0; msk = p.mask0;
+    } else {
+        off = m * (p.N - p.n0) + (n - p.n0);
+        dst = p.dst1; msk = p.mask1;
+    }
+    v0 += b0;
+    v1 += b1;
+    if (p.resid) {
+        const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.resid + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v0[e] += (float)r[e]; v1[e] += (float)r[4 + e]; }
+    }
+    if (p.flags & PU_EPI_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v0[e] = fmaxf(v0[e], 0.f); v1[e] = fmaxf(v1[e], 0.f); }
+    }
+    if (p.mask0 || p.mask1) {
+        const __bf16* mp = msk ? msk + off : (p.mask0 ? p.mask0 : p.mask1);
+        const bf16x8 mv = *reinterpret_cast<const bf16x8*>(mp);
+        if (msk) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (!((float)mv[e] > 0.f)) v0[e] = 0.f;
+                if (!((float)mv[4 + e] > 0.f)) v1[e] = 0.f;
+            }
+        }
+    }
+    if (p.flags & PU_EPI_ACCUM) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(dst + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v0[e] += (float)a[e]; v1[e] += (float)a[4 + e]; }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { o[e] = (__bf16)v0[e]; o[4 + e] = (__bf16)v1[e]; }
+    *reinterpret_cast<bf16x8*>(dst + off) = o;
+}
+
+// s_waitcnt vmcnt(base + extra) for a run-time extra in {0, 2, ..., 62 - base} (wave-uniform);
+// anything else waits for vmcnt(base) (more than needed: always safe)
+template <int BASE, int X = 0>
+__device__ __forceinline__ void wait_vm_plus(int extra) {
+    if constexpr (BASE + X <= 63) {
+        if (extra == X) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BASE + X) : "memory");
+            return;
+        }
+        wait_vm_plus<BASE, X + 2>(extra);
+    } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BASE) : "memory");
+    }
+}
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 __device__ __attribute__((aligned(16))) __bf16 g_zero_b16[8];
@@ -649,6 +718,229 @@ __global__ __launch_bounds__(HB_NT) __attribute__((amdgpu_waves_per_eu(2))) void
     }
 }
 
+// ---------------------------------------------------------------- halo bf16 kernel, DMA ring
+// The same convolutions as igemm_bf16_halo_kernel (3x3 / s1 / p1, width 32 / 64 / 128), restaged so
+// that nothing waits on HBM: PMC on the register-staged kernel showed MFMA busy 0.21 and waves
+// parked on s_waitcnt / barriers 49 % of their cycles - its next group's halo was loaded one group
+// ahead through registers, then stored to LDS between two barriers.
+//   block: 4 waves (one per SIMD), one block per CU, persistent over an XCD-contiguous tile range;
+//     tile = 512 output pixels (R = 512 / W whole rows of one image) x 64 output channels;
+//     wave = 128 pixels x 64 channels (4 x 2 fragments: 6 fragment reads per 8 MFMAs);
+//   stage = 16 input channels: the (R+2) x (W+2) halo [pixel][16 ch] (32 B per pixel: a 32-pixel
+//     fragment is one contiguous 1 KB run at every tap shift - conflict-free) and the 9 tap slices
+//     of the weights [tap][n][16 k], both written straight into LDS by buffer_load ... lds (32-bit
+//     offsets: per-lane pixel index x the source's pixel stride + a scalar channel offset; padding
+//     and out-of-image pixels get an out-of-range offset and land as zeros);
+//   3-slot ring, loads issued two stages ahead (the next tile's first stages fly over this tile's
+//     last MFMAs and its epilogue), one counted vmcnt + one barrier per stage.
+// K order: group g (32 channels), half h, tap t - a different summation order from the per-tap
+// kernels (fp32 accumulation of exact bf16 products either way).  Host: halo2_ok_b.
+constexpr int H2_NT = 256;
+constexpr int H2_BN = 64;
+#ifndef PU_H2_ABL
+#define PU_H2_ABL 0     // ablation builds only (timing): 1 no halo loads, 2 no weight loads, 3 neither
+#endif
+
+template <int W>
+__global__ __launch_bounds__(H2_NT) void igemm_bf16_halo2_kernel(const IgemmBf16Params p) {
+    constexpr int R = 512 / W;
+    constexpr int HW = W + 2;
+    constexpr int HP = (R + 2) * HW;                  // halo pixels
+    constexpr int HI = (HP * 2 + 63) / 64;            // 1 KB DMA instructions for the halo
+    constexpr int XB = HI * 1024;                     // halo bytes (padded to whole instructions)
+    constexpr int WI = 9 * H2_BN * 2 / 64;            // weight instructions: 18
+    constexpr int STAGE = XB + WI * 1024;
+    constexpr int HPW = (HI + 3) / 4;                 // per wave
+    constexpr int WPW = (WI + 3) / 4;
+    constexpr int LPW = HPW + WPW;                    // loads per wave per stage (dummies included)
+    constexpr int FRAGS = 4;                          // 32-pixel fragments per wave
+    static_assert(R * W == 512 && W % 32 == 0 && 3 * STAGE + 1024 <= 160 * 1024, "halo2 tile");
+
+    extern __shared__ __attribute__((aligned(1024))) char h2_lds[];
+    char* sink = h2_lds + 3 * STAGE;                  // dummy DMA target
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const int ntiles = p.M / 512 * p.gn;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
+    const int tq = (ntiles + 7) >> 3;
+    const int t_end = min(ntiles, (xcd + 1) * tq);
+    const int t_first = xcd * tq + (int)(blockIdx.x >> 3);
+    if (t_first >= t_end) return;                      // uniform per block
+    const int rb = p.Ho / R;
+    const int S = p.C / 16;                            // stages per tile
+    const unsigned wbytes = (unsigned)p.N * (unsigned)p.k_pad * 2u;
+    const unsigned x0bytes = (unsigned)p.in_pix * (unsigned)p.c0 * 2u;
+    const unsigned x1bytes = (unsigned)p.in_pix * (unsigned)p.c1 * 2u;
+
+    // ---- loader state (the stage being issued may belong to the next tile)
+    int ld_tile = t_first, ld_s = 0;
+    int hpix[HPW];                                     // image pixel of this lane's halo piece, -1: zero
+    unsigned hchunk[HPW];
+    unsigned wvo[WPW];                                 // weight byte offset (without the stage's k)
+    auto setup = [&](int t) {
+        const int mt = t / p.gn;
+        const int b = mt / rb;
+        const int r0 = (mt - b * rb) * R;
+#pragma unroll
+        for (int j = 0; j < HPW; ++j) {
+            const int I = wave + 4 * j;
+            const int e = I * 64 + lane;
+            const int hp = e >> 1;
+            const int hr = hp / HW, hc = hp - hr * HW;
+            const int ir = r0 - 1 + hr, ic = hc - 1;
+            const bool ok = I < HI && hp < HP && (unsigned)ir < (unsigned)p.Hi && (unsigned)ic < (unsigned)W;
+            hpix[j] = ok ? (b * p.Hi + ir) * W + ic : -1;
+            hchunk[j] = (unsigned)(e & 1) * 16u;
+        }
+        const int n_blk = (t - mt * p.gn) * H2_BN;
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) {
+            const int I = wave + 4 * j;
+            const int e = I * 64 + lane;
+            const int tap = e >> 7, n = (e >> 1) & 63, ch = e & 1;
+            wvo[j] = I < WI ? (unsigned)((n_blk + n) * p.k_pad + tap * 32 + ch * 8) * 2u : LEAN_OOB;
+        }
+    };
+    auto issue = [&](int slot) {
+        const bool live = ld_tile < t_end;
+        char* base = h2_lds + slot * STAGE;
+        const int g = ld_s >> 1, h = ld_s & 1;
+        const int c = g * 32 + h * 16;
+        const bool second = c >= p.c0;
+        const __bf16* src = second ? p.src1 : p.src0;
+        const unsigned cs2 = (unsigned)(second ? p.c1 : p.c0) * 2u;
+        const unsigned xbytes = live ? (second ? x1bytes : x0bytes) : 0u;
+        const unsigned soff = (unsigned)(second ? c - p.c0 : c) * 2u;
+#pragma unroll
+        for (int j = 0; j < HPW; ++j) {
+            const int I = wave + 4 * j;
+            const unsigned vo = hpix[j] >= 0 ? (unsigned)hpix[j] * cs2 + hchunk[j] : LEAN_OOB;
+            if (PU_H2_ABL != 1 && PU_H2_ABL != 3) lean_load(src, xbytes, I < HI ? base + I * 1024 : sink, vo, soff);
+        }
+        const unsigned wsoff = (unsigned)(g * 288 + h * 16) * 2u;
+#pragma unroll
+        for (int j = 0; j < WPW; ++j) {
+            const int I = wave + 4 * j;
+            if (PU_H2_ABL != 2 && PU_H2_ABL != 3)
+                lean_load(p.wt, live ? wbytes : 0u, I < WI ? base + XB + I * 1024 : sink, wvo[j], wsoff);
+        }
+        if (++ld_s == S) {                             // the next stage opens the next tile
+            ld_s = 0;
+            ld_tile += per_xcd;
+            if (ld_tile < t_end) setup(ld_tile);
+        }
+    };
+
+    // ---- fragment addresses: fragment i = pixels wave*128 + 32 i .. +31 (one image row each)
+    unsigned xa[FRAGS];
+#pragma unroll
+    for (int i = 0; i < FRAGS; ++i) {
+        const int p0 = wave * 128 + 32 * i;
+        const int orow = p0 / W, ocol = p0 - orow * W;
+        xa[i] = (unsigned)((orow * HW + ocol + lr) * 32 + lh * 16);
+    }
+    const unsigned wa = (unsigned)(XB + lr * 32 + lh * 16);
+
+    // memory operations per wave of one tile's epilogue: 4 fragments x 4 pixel passes x epi8_ops,
+    // plus the two bias loads
+    const int EOPS = 16 * epi8_ops(p) + (p.bias ? 2 : 0);
+    setup(t_first);
+    issue(0);
+    issue(1);
+    int tile = t_first;
+    int u = 0;                                         // stage counter (ring position)
+    for (;;) {
+        const int mt = tile / p.gn;
+        const int m_blk = mt * 512;
+        const int n_blk = (tile - mt * p.gn) * H2_BN;
+        f32x16 acc[FRAGS][2];
+#pragma unroll
+        for (int i = 0; i < FRAGS; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int s = 0; s < S; ++s, ++u) {
+            // stage u landed.  In a tile's first two stages the previous tile's epilogue (EOPS
+            // memory operations, issued after stage u+1's loads) is still in flight: count it
+            // instead of draining it, so its stores overlap this tile's MFMAs
+            if (s < 2 && tile != t_first) wait_vm_plus<LPW>(EOPS);
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPW) : "memory");
+            __builtin_amdgcn_s_barrier();              // ... for every wave; slot (u+2)%3 is free
+            asm volatile("" ::: "memory");
+            const int slot = u % 3;
+            issue(slot == 0 ? 2 : slot - 1);
+            const char* a = h2_lds + slot * STAGE;
+            // fragments double-buffered one tap ahead; the scheduling barriers keep tap t+1's six
+            // reads ahead of tap t's eight MFMAs (left alone, the scheduler interleaved each read
+            // with its consumer: one wave per SIMD then waits out every LDS latency)
+            bf16x8 fx[2][FRAGS], fw[2][2];
+            auto frag = [&](int t, int bsel) {
+                const int toff = ((t / 3) * HW + (t % 3)) * 32;
+#pragma unroll
+                for (int i = 0; i < FRAGS; ++i) fx[bsel][i] = *reinterpret_cast<const bf16x8*>(a + xa[i] + toff);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    fw[bsel][j] = *reinterpret_cast<const bf16x8*>(a + wa + (t * H2_BN + j * 32) * 32);
+            };
+            frag(0, 0);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                if (t + 1 < 9) frag(t + 1, (t + 1) & 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < FRAGS; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[t & 1][j], fx[t & 1][i], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // epilogue through the ring slot this stage just consumed (free until the next stage's
+        // issue, which follows a barrier): per 32-pixel fragment, the wave's 32 x 64 fp32 tile
+        // goes to LDS [pixel][68 floats] (conflict-free b128 writes), and comes back as 8
+        // channels of one pixel per lane - every store is a full 128-byte pixel row segment
+        // (the MFMA layout would store 8 bytes per lane and 64 pieces per instruction)
+        __builtin_amdgcn_s_barrier();                  // every wave is done reading the slot
+        asm volatile("" ::: "memory");
+        float* ep = reinterpret_cast<float*>(h2_lds + ((u - 1) % 3) * STAGE) + wave * (32 * 68);
+        const int rp = lane >> 3, c8 = (lane & 7) * 8;  // read-back: pixel rp (+8 per pass), channels c8..
+        f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+        if (p.bias) {
+            b0 = *reinterpret_cast<const f32x4*>(p.bias + n_blk + c8);
+            b1 = *reinterpret_cast<const f32x4*>(p.bias + n_blk + c8 + 4);
+        }
+#pragma unroll
+        for (int i = 0; i < FRAGS; ++i) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f32x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                    *reinterpret_cast<f32x4*>(ep + lr * 68 + j * 32 + 8 * q + 4 * lh) = v;
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own wave's tile only: no barrier
+#pragma unroll
+            for (int ps = 0; ps < 4; ++ps) {
+                const int px = ps * 8 + rp;
+                const f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + px * 68 + c8);
+                const f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + px * 68 + c8 + 4);
+                epi_store8_b(p, (long long)(m_blk + wave * 128 + i * 32 + px), n_blk + c8, v0, v1, b0, b1);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next fragment's writes
+        }
+        tile += per_xcd;
+        if (tile >= t_end) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing (dead) loads drain before exit
+}
+
 __global__ __launch_bounds__(256) void igemm_bf16_splitk_epilogue_kernel(const IgemmBf16Params p) {
     const int nq = p.N >> 2;
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -712,6 +1004,23 @@ static int device_cus_b() {
         cus[dev] = (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8) ? n : 256;
     }
     return cus[dev];
+}
+
+// the DMA-ring halo kernel: the halo kernel's shapes with 512-pixel row blocks (R = 512 / W rows);
+// PU_CONV_HALO_V1 keeps the register-staged kernel (A/B runs, its bit-identity test)
+static bool halo2_ok_b(const pu_conv_args* a) {
+    // its epilogue stores 8 channels (16 B) per lane: 8-channel split point, 16-byte-aligned tensors
+    const uintptr_t ae = (uintptr_t)a->dst0 | (uintptr_t)a->dst1 | (uintptr_t)a->mask0 | (uintptr_t)a->mask1 |
+                         (uintptr_t)a->resid;
+    return halo_ok_b(a) && !(a->flags & PU_CONV_HALO_V1) && a->out_h % (512 / a->out_w) == 0 && a->n0 % 8 == 0 &&
+           (ae & 15) == 0;
+}
+
+template <int W>
+static size_t halo2_lds_bytes() {
+    constexpr int HP = (512 / W + 2) * (W + 2);
+    constexpr int STAGE = (HP * 2 + 63) / 64 * 1024 + 18 * 1024;
+    return 3 * STAGE + 1024;
 }
 
 // the lean kernel: 3x3, 32-channel K groups, one pixel stride for both sources, K == k_pad,
@@ -817,6 +1126,21 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
     if (st != PU_OK) return st;
     const int N = a->n;
     hipStream_t s = as_stream(stream);
+    if (halo2_ok_b(a)) {
+        p.ksplit = 1;
+        p.gn = N / H2_BN;
+        const long long tiles = M / 512 * p.gn;
+        const long long per_xcd = ceil_div(tiles, 8LL);
+        const int blocks_per_xcd = device_cus_b() / 8;        // one block per CU
+        const dim3 hgrid((unsigned)(8 * (per_xcd < blocks_per_xcd ? per_xcd : blocks_per_xcd)));
+        if (a->out_w == 128)
+            hipLaunchKernelGGL((igemm_bf16_halo2_kernel<128>), hgrid, dim3(H2_NT), halo2_lds_bytes<128>(), s, p);
+        else if (a->out_w == 64)
+            hipLaunchKernelGGL((igemm_bf16_halo2_kernel<64>), hgrid, dim3(H2_NT), halo2_lds_bytes<64>(), s, p);
+        else
+            hipLaunchKernelGGL((igemm_bf16_halo2_kernel<32>), hgrid, dim3(H2_NT), halo2_lds_bytes<32>(), s, p);
+        return check_launch("pu_conv_igemm_bf16 (halo2)");
+    }
     if (halo_ok_b(a)) {
         p.ksplit = 1;
         p.gn = N / HB_BN;
@@ -863,6 +1187,13 @@ extern "C" int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, 
     int st = setup_bf16(a, &p, &M);
     if (st != PU_OK) return st;
     int ks, tp;
+    if (halo2_ok_b(a)) {              // the DMA-ring halo kernel: 512 pixels x 64 channels
+        *bm = 512;
+        *bn = H2_BN;
+        if (ksplit) *ksplit = 1;
+        if (kind) *kind = 2;
+        return PU_OK;
+    }
     if (halo_ok_b(a)) {               // the halo kernel: 256 pixels x 64 channels, no split
         *bm = 256;
         *bn = HB_BN;

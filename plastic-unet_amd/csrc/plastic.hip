@@ -169,6 +169,15 @@ constexpr int FH_NT = 512;    // threads per block (2 blocks per CU at nbf 128: 
                                // loads overlap the other's GEMM / trace phases)
 constexpr int FH_WAVES = FH_NT / 64;
 constexpr int FH_LDS_W = 16384;   // floats of the Weff chunk (64 KB)
+#ifndef PU_FH_ABL
+#define PU_FH_ABL 0               // ablation builds only: 1 = stop after the outconv phase
+#endif
+#ifndef PU_FH_LDS_MIN
+#define PU_FH_LDS_MIN 0           // ablation builds only: pad the LDS request (blocks per CU)
+#endif
+#ifndef PU_FH_U
+#define PU_FH_U 8                 // pixels per lane group in flight (L >= 8)
+#endif
 
 // Weff rows per LDS chunk: all N rows when N x N fits, else the largest multiple of 4 (the MFMA's
 // k step) that divides N and fits (N % 16 == 0, so 16 always qualifies: N = 144 -> 72, 192 -> 64,
@@ -192,7 +201,7 @@ __device__ __forceinline__ f32x4 fh_ld4<__bf16>(const __bf16* p) {
     return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
 
-template <typename T, int L, int TPW, bool PIPE>
+template <typename T, int L, int TPW>
 __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ wo,
                                                                const float* __restrict__ bo, int C,
                                                                const float* __restrict__ H, const float* __restrict__ w,
@@ -213,77 +222,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     const float* Hb = H + (long long)b * nn;
 
     // ---- 1. outconv
-    if constexpr (PIPE) {
-        // C == 4 L (one float4 per lane and pixel) and all of Weff in one LDS chunk: the feature
-        // loads of pass p + 1 are in flight while pass p is reduced (two register sets), and one
-        // float4 of w / alpha / H (Weff piece p) rides along with every pass, so the Weff build
-        // costs no round trips of its own.  Same arithmetic as the loop below (bit-identical).
-        constexpr int U = L >= 8 ? 8 : 4;
-        constexpr int PPP = FH_NT / L;
-        constexpr int PER = U * PPP;
-        const float bias = bo ? bo[0] : 0.f;
-        const int lane = tid % L;
-        const int npix = (fuse ? FH_R + 1 : FH_R) * N;
-        const int npass = (npix + PER - 1) / PER;
-        const int nw4 = N * N / 4;
-        const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + lane * 4);
-        f32x4 va[U], vb[U];
-        f32x4 pw, pa, ph;
-        auto load = [&](f32x4 (&v)[U], int p) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int q = min(p * PER + tid / L + u * PPP, npix - 1);
-                const int r = (int)fdiv((unsigned)q, dN), k = q - r * N;
-                v[u] = fh_ld4<T>(fb + ((long long)(r < FH_R ? i0 + r : 0) * N + k) * C + lane * 4);
-            }
-        };
-        auto load_piece = [&](int p) {
-            const int e4 = min(p * FH_NT + tid, nw4 - 1);
-            pw = reinterpret_cast<const f32x4*>(w)[e4];
-            pa = reinterpret_cast<const f32x4*>(alpha)[e4];
-            ph = reinterpret_cast<const f32x4*>(Hb)[e4];
-        };
-        auto store_piece = [&](int p) {
-#pragma clang fp contract(off)
-            const int e4 = p * FH_NT + tid;
-            if (e4 < nw4) {
-                f32x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = pw[e] + pa[e] * ph[e];     // torch: w + mul(alpha, hebb)
-                reinterpret_cast<f32x4*>(ws)[e4] = o;
-            }
-        };
-        auto reduce = [&](f32x4 (&v)[U], int p) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                float t = 0.f;
-                t += dot4_fma(v[u], ww);
-                if (L >= 16) t += __shfl_xor(t, 8, 16);
-                if (L >= 8) t += __shfl_xor(t, 4, 16);
-                if (L >= 4) t += __shfl_xor(t, 2, 16);
-                if (L >= 2) t += __shfl_xor(t, 1, 16);
-                const int q = p * PER + tid / L + u * PPP;
-                if (lane == 0 && q < npix) xs[q] = t + bias;
-            }
-        };
-        load(va, 0);
-        for (int p = 0; p < npass; p += 2) {
-            if (p + 1 < npass) load(vb, p + 1);
-            load_piece(p);
-            reduce(va, p);
-            store_piece(p);
-            if (p + 1 < npass) {
-                if (p + 2 < npass) load(va, p + 2);
-                load_piece(p + 1);
-                reduce(vb, p + 1);
-                store_piece(p + 1);
-            }
-        }
-        for (int p = npass; p * FH_NT < nw4; ++p) {
-            load_piece(p);
-            store_piece(p);
-        }
-    } else {
+    {
         constexpr int U = L >= 8 ? 8 : 4;       // pixels per lane group in flight
         const float bias = bo ? bo[0] : 0.f;
         const int lane = tid % L;
@@ -323,6 +262,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     __syncthreads();
     // X rows of this block -> global (coalesced)
     for (int e = tid; e < FH_R * N; e += FH_NT) X[(long long)b * nn + (long long)i0 * N + e] = xs[e];
+    if (PU_FH_ABL == 1) return;
 
     // the trace update's first float4 of H (rows i0.., L2-resident after the Weff build), in
     // flight during the GEMM
@@ -337,24 +277,34 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float acc0 = 0.f;                                  // y0 chain of column tid (tid < N)
     for (int k0 = 0; k0 < N; k0 += kc) {
-        if (!PIPE) {
+        {
 #pragma clang fp contract(off)
-            const int ne = kc * N;
-            for (int e0 = tid; e0 < ne; e0 += 8 * FH_NT) {
-                float wv[8], av[8], hv[8];
+            // float4 pieces, 8 per array and thread in flight at once (N = 128: the whole chunk in
+            // one round trip; the scalar form took four, 4.4 us of the kernel by ablation)
+            const int ne4 = kc * N / 4;
+            const f32x4* w4 = reinterpret_cast<const f32x4*>(w + (long long)k0 * N);
+            const f32x4* a4 = reinterpret_cast<const f32x4*>(alpha + (long long)k0 * N);
+            const f32x4* h4 = reinterpret_cast<const f32x4*>(Hb + (long long)k0 * N);
+            for (int e0 = tid; e0 < ne4; e0 += 8 * FH_NT) {
+                f32x4 wv[8], av[8], hv[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    const long long o = (long long)k0 * N + min(e0 + FH_NT * u, ne - 1);
-                    wv[u] = w[o]; av[u] = alpha[o]; hv[u] = Hb[o];
+                    const int o = min(e0 + FH_NT * u, ne4 - 1);
+                    wv[u] = w4[o]; av[u] = a4[o]; hv[u] = h4[o];
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
-                    if (e0 + FH_NT * u < ne) ws[e0 + FH_NT * u] = wv[u] + av[u] * hv[u];   // torch: w + mul(alpha, hebb)
+                    if (e0 + FH_NT * u < ne4) {
+                        f32x4 o;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) o[c] = wv[u][c] + av[u][c] * hv[u][c];   // torch: w + mul(alpha, hebb)
+                        reinterpret_cast<f32x4*>(ws)[e0 + FH_NT * u] = o;
+                    }
             }
         }
         __syncthreads();
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
+        for (int t = 0; t < TPW && PU_FH_ABL != 2; ++t) {
             const int tile = wave + FH_WAVES * t;
             if (tile < tiles) {
                 const float* wcol = ws + (l >> 4) * N + tile * 16 + (l & 15);
@@ -363,7 +313,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
                     acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xrow[kk], wcol[kk * N], acc[t], 0, 0, 0);
             }
         }
-        if (fuse && tid < N) {
+        if (fuse && tid < N && PU_FH_ABL != 2) {
             float s0 = acc0;
             for (int kk = 0; kk < kc; ++kk) s0 = fmaf(xs[FH_R * N + k0 + kk], ws[kk * N + tid], s0);
             acc0 = s0;
@@ -371,6 +321,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
         __syncthreads();
     }
 
+    if (PU_FH_ABL == 3) return;
     // ---- 3. sigmoid + store (C layout of 16x16: column l & 15, rows 4 (l >> 4) + reg)
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
@@ -384,7 +335,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
             }
         }
     }
-    if (!fuse) return;
+    if (!fuse || PU_FH_ABL == 4) return;
     if (tid < N) y0s[tid] = 1.f / (1.f + expf(-acc0));
     __syncthreads();
 
@@ -673,21 +624,16 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
     const int q = C / 4;
     const int L = q >= 16 ? 16 : (q & (q - 1)) == 0 ? q : 16;    // lanes per pixel
     const int kc = fused_head_chunk(N);                           // Weff rows per LDS chunk
-    const bool pipe = C == 4 * L && kc == N;
-    const size_t lds = ((size_t)(FH_R + 1) * N + (size_t)kc * N + N) * sizeof(float);
+    size_t lds = ((size_t)(FH_R + 1) * N + (size_t)kc * N + N) * sizeof(float);
+    if (lds < (size_t)PU_FH_LDS_MIN) lds = PU_FH_LDS_MIN;
     const dim3 grid(N / FH_R, a->batch);
     const FastDiv dN = make_fastdiv(N);
     hipStream_t s = as_stream(stream);
     const int tpw = (N / 16 + FH_WAVES - 1) / FH_WAVES;           // column tiles per wave
-#define PU_FH3(T_, L_, W_, P_)                                                                                     \
-    hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_, P_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat,     \
+#define PU_FH2(T_, L_, W_)                                                                                     \
+    hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat,     \
                        a->out_w, a->out_b, C, a->hebb, a->w, a->alpha, a->eta, a->x, a->y, a->hebb_out, N, dN, kc, \
                        a->rule)
-#define PU_FH2(T_, L_, W_)                                                                                     \
-    do {                                                                                                       \
-        if (pipe) PU_FH3(T_, L_, W_, true);                                                                    \
-        else PU_FH3(T_, L_, W_, false);                                                                        \
-    } while (0)
 #define PU_FH(T_, L_)                                                                                       \
     do {                                                                                                    \
         if (tpw <= 1) PU_FH2(T_, L_, 1);                                                                    \
@@ -706,7 +652,6 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
 #undef PU_FH_L
 #undef PU_FH
 #undef PU_FH2
-#undef PU_FH3
     return check_launch("pu_plastic_head_fwd");
 }
 

@@ -868,19 +868,26 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
 
     const int ntiles = p.batch * p.tiles_h * p.tiles_w;
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // the tile's halo and gradient rows are loaded into registers one tile ahead (all loads of a
+    // tile in flight at once), stored to LDS between two barriers, and the next tile's loads then
+    // fly under this tile's accumulation
+    constexpr int NH = HH * HWD * C4, NG = SW_TH * SW_TW * N4;
+    constexpr int PH = (NH + 255) / 256, PG2 = (NG + 255) / 256;
+    f32x4 rh[PH], rg[PG2];
+    auto load_tile = [&](int t) {
         const int txi = t % p.tiles_w;
         const int tyi = (t / p.tiles_w) % p.tiles_h;
         const int b = t / (p.tiles_w * p.tiles_h);
         const int y0 = tyi * SW_TH, x0 = txi * SW_TW;
         const long long img = (long long)b * p.Hi * p.Wi;
-        __syncthreads();                       // previous tile's readers are done
-        for (int e = tid; e < HH * HWD * C4; e += 256) {
+#pragma unroll
+        for (int it = 0; it < PH; ++it) {
+            const int e = it * 256 + tid;
             const int q = e % C4, pix = e / C4;
             const int hx = pix % HWD, hy = pix / HWD;
             const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
+            if (e < NH && (unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
                 const long long px = img + (long long)gy * p.Wi + gx;
                 if (C % 4 == 0 && p.c0 % 4 == 0) {
                     const int c = 4 * q;
@@ -894,16 +901,33 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
                     }
                 }
             }
-            *reinterpret_cast<f32x4*>(halo + pix * CP + 4 * q) = v;
+            rh[it] = v;
         }
-        for (int e = tid; e < SW_TH * SW_TW * N4; e += 256) {
+#pragma unroll
+        for (int it = 0; it < PG2; ++it) {
+            const int e = it * 256 + tid;
             const int q = e % N4, pix = e / N4;
             const int oy = y0 + pix / SW_TW, ox = x0 + pix % SW_TW;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (oy < p.Ho && ox < p.Wo)
+            if (e < NG && oy < p.Ho && ox < p.Wo)
                 v = *reinterpret_cast<const f32x4*>(p.P + ((long long)(b * p.Ho + oy) * p.Wo + ox) * N + 4 * q);
-            *reinterpret_cast<f32x4*>(gt + pix * N + 4 * q) = v;
+            rg[it] = v;
         }
+    };
+    if ((int)blockIdx.x < ntiles) load_tile(blockIdx.x);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        __syncthreads();                       // previous tile's readers are done
+#pragma unroll
+        for (int it = 0; it < PH; ++it) {
+            const int e = it * 256 + tid;
+            if (e < NH) *reinterpret_cast<f32x4*>(halo + (e / C4) * CP + 4 * (e % C4)) = rh[it];
+        }
+#pragma unroll
+        for (int it = 0; it < PG2; ++it) {
+            const int e = it * 256 + tid;
+            if (e < NG) *reinterpret_cast<f32x4*>(gt + (e / N4) * N + 4 * (e % N4)) = rg[it];
+        }
+        if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
         __syncthreads();
         if (active) {
             if (wi) {

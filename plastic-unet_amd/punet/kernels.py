@@ -10,7 +10,7 @@ import torch
 
 from . import _lib
 from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, check,
-                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO)
+                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
@@ -31,16 +31,22 @@ _MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem"}
 _FP32_MATH = os.environ.get("PU_FP32_MATH", "split6")
 
 
-# bf16 3x3/s1 convolutions of width 32/64/128 on the halo kernel (default) or the per-tap lean
-# kernel (PU_CONV_HALO=0: A/B runs; tests flip it with set_conv_halo)
-_CONV_HALO = os.environ.get("PU_CONV_HALO", "1") != "0"
+# bf16 3x3/s1 convolutions of width 32/64/128: 2 = the DMA-ring halo kernel (512-pixel
+# row blocks), 1 = the register-staged halo kernel (default), 0 = the per-tap lean kernel (PU_CONV_HALO:
+# A/B runs; tests flip it with set_conv_halo)
+_CONV_HALO = int(os.environ.get("PU_CONV_HALO", "1"))
 
 
-def set_conv_halo(on):
-    """Route eligible bf16 convolutions to the halo kernel (True) or the per-tap kernel.  Returns the previous setting."""
+def set_conv_halo(mode):
+    """Route eligible bf16 convolutions: 2 (or True) DMA-ring halo kernel, 1 register-staged halo
+    kernel, 0 (or False) per-tap kernel.  Returns the previous setting."""
     global _CONV_HALO
-    prev, _CONV_HALO = _CONV_HALO, bool(on)
+    prev, _CONV_HALO = _CONV_HALO, (2 if mode is True else 0 if mode is False else int(mode))
     return prev
+
+
+def _halo_flags():
+    return {2: 0, 1: PU_CONV_HALO_V1}.get(_CONV_HALO, PU_CONV_NO_HALO)
 
 
 def fp32_math():
@@ -165,7 +171,7 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
         _req(t, nm, dt)
     _req(bias, "bias")
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
-        | (PU_EPI_RESID if resid is not None else 0) | (0 if _CONV_HALO else PU_CONV_NO_HALO)
+        | (PU_EPI_RESID if resid is not None else 0) | _halo_flags()
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,

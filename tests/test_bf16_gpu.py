@@ -188,7 +188,7 @@ def test_unetp_bf16_vs_fp64_oracle():
 
 @pytest.mark.parametrize("c0,cout", [(32, 64), (64, 64)])
 def test_bf16_halo_conv_bit_identical_to_lean(c0, cout):
-    """the halo kernel sums the same bf16 products in the same order as the per-tap lean kernel
+    """the register-staged halo kernel sums the same bf16 products in the same order as the per-tap lean kernel
     (unsplit at 8 x 128 x 128: 512 tiles), so forward and dgrad outputs are bit-identical"""
     B, H = 8, 128
     g = torch.Generator(device=DEV).manual_seed(c0 + cout)
@@ -197,9 +197,9 @@ def test_bf16_halo_conv_bit_identical_to_lean(c0, cout):
     b = torch.randn(cout, device=DEV, generator=g)
     dz = torch.randn(B, H, H, cout, device=DEV, generator=g).to(BF)
     outs = []
-    prev = K.set_conv_halo(True)
+    prev = K.set_conv_halo(1)
     try:
-        for halo in (True, False):
+        for halo in (1, 0):               # register-staged halo kernel vs per-tap
             K.set_conv_halo(halo)
             pk = T._Packs()
             y = T.conv3x3(x, w, b, pk)
@@ -210,3 +210,42 @@ def test_bf16_halo_conv_bit_identical_to_lean(c0, cout):
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("B,H,c0,c1,cout", [(8, 128, 64, 0, 64), (4, 128, 32, 32, 128), (8, 64, 128, 0, 64),
+                                            (16, 32, 64, 64, 192), (3, 32, 96, 0, 64)])
+def test_bf16_halo2_conv_matches_fp32_and_halo1(B, H, c0, c1, cout):
+    """the DMA-ring halo kernel (512-pixel row blocks, 16-channel stages, K order group/half/tap)
+    sums the same exact bf16 products as the register-staged kernel in another order: fwd and
+    dgrad outputs within 1 bf16 ulp of it, and within the bf16 tolerance of torch fp32 on the
+    bf16-rounded operands"""
+    g = torch.Generator(device=DEV).manual_seed(H + c0 + c1 + cout)
+    x0 = torch.randn(B, H, H, c0, device=DEV, generator=g).relu().to(BF)
+    x1 = torch.randn(B, H, H, c1, device=DEV, generator=g).relu().to(BF) if c1 else None
+    w = torch.randn(cout, c0 + c1, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(cout, device=DEV, generator=g)
+    dz = torch.randn(B, H, H, cout, device=DEV, generator=g).to(BF)
+    outs = []
+    prev = K.set_conv_halo(2)
+    try:
+        for halo in (2, 1):
+            K.set_conv_halo(halo)
+            pk = T._Packs()
+            y = T.conv3x3(x0, w, b, pk, x1=x1)
+            d0, d1 = T.conv3x3_dgrad(dz, w, pk, split=c0 if c1 else None, mask0=x0, mask1=x1)
+            outs.append((y, d0, d1))
+    finally:
+        K.set_conv_halo(prev)
+    torch.cuda.synchronize()
+    for a, r in zip(outs[0], outs[1]):
+        if a is None:
+            continue
+        diff = (a.float() - r.float()).abs()
+        # one bf16 ulp (8-bit significand) of the larger of the two - a sum within fp32 noise of a
+        # rounding midpoint rounds up in one order and down in the other - plus the fp32
+        # accumulation noise of a cancelling sum (results near 1e-6 from terms near 0.05)
+        ulp = torch.maximum(a.float().abs(), r.float().abs()) * 2.0 ** -7
+        assert bool((diff <= ulp + 1e-4).all()), diff.max().item()
+    xc = torch.cat([x0, x1], 3) if c1 else x0
+    ref = torch.relu(F.conv2d(nchw(xc.float()), rb(w), b, padding=1))
+    close_bf16(nchw(outs[0][0]), ref)
