@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PU_ABI_VERSION 1
+#define PU_ABI_VERSION 2
 
 typedef enum {
     PU_OK = 0,
@@ -123,9 +123,29 @@ typedef struct {
      * dropped terms < 2^-23 relative) on v_mfma_f32_32x32x16_bf16 - 2.7x the fp32-MFMA rate.
      * Layers that take another kernel (small-channel direct, odd channel counts) use `weight`. */
     const void* weight6;
+    /* optional: the Winograd F(2x2,3x3) operand U of `weight` (pu_pack_wino; fwd for a forward
+     * conv, dgrad for the data gradient).  When set together with weight6, a 3x3/s1/p1 layer on an
+     * even same-size grid with 16-channel chunks (c1 == 0 or c1 == c0, c0 + c1 a multiple of 32),
+     * n a multiple of 64 and the float4 epilogue runs as 16 element-wise GEMMs over the transformed
+     * tiles (2.25x fewer products; same 6-product fp32 arithmetic, fp32 transforms) */
+    const void* wino;
 } pu_conv_args;
 
 int pu_conv_igemm(const pu_conv_args* a, void* stream);
+/* Winograd operand U = G g G^T of a 3x3 conv weight w[cout][cin][3][3] (fp32, OIHW):
+ *   fwd   (dgrad = 0): n = cout output channels, reduced over c = cin
+ *   dgrad (dgrad = 1): n = cin, c = cout, g = the flipped kernel w[c][n][2-r][2-s]
+ * formed in fp64, rounded to fp32, split exactly into hi/mid/lo bf16 planes, laid out
+ * [c/16][16 positions][3 planes][n][16 channels] (pu_wino_bytes(n, c) bytes; c % 16 == 0).
+ * All jobs in one launch (re-packed after every optimizer step). */
+typedef struct {
+    const float* w;
+    void* out;
+    int cout, cin;
+    int dgrad;
+} pu_wino_job;
+size_t pu_wino_bytes(int n, int c);
+int pu_pack_wino(const pu_wino_job* jobs, int n_jobs, void* stream);
 /* packed fp32 weight [n][k_pad] -> bf16 planes [k_pad/16][6][n][8] (q = plane*2 + (k%16)/8; plane
  * 0/1/2 = hi/mid/lo, w == hi + mid + lo exactly); out holds n*k_pad*3 bf16 (6 bytes per weight) */
 int pu_split_weight6(const float* packed, void* out, int n, int k_pad, void* stream);

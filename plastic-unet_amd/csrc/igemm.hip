@@ -11,42 +11,18 @@
 // (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA blocks.  Each lane reads 4 consecutive k of one row with
 // a single ds_read_b128 and feeds them to 4 MFMAs: for MFMA step s, lane (i, h) supplies
 // A[i][kk*8 + 4h + s] and B[kk*8 + 4h + s][j] - the same k on both operands, so the sum is exact.
-#include "common.h"
+#include "conv_common.h"
 #include <type_traits>
 
 
 namespace pu {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int IG_BK = 16;
 constexpr int IG_LDS = IG_BK + 4;
 
 enum { LOAD_CHUNK16 = 0, LOAD_VEC4 = 1, LOAD_SCALAR = 2 };
 
-struct IgemmParams {
-    int M, N, K, k_pad;
-    int Hi, Wi, Ho, Wo, kh, kw, stride, pad;
-    int C, c0, c1;
-    const float* src0;
-    const float* src1;
-    const float* wt;
-    const float* bias;
-    float* dst0;
-    float* dst1;
-    const float* mask0;
-    const float* mask1;
-    int n0, flags;
-    int cgroup, taps, gn;   // K order (0 tap-major, 16/32 channel-group-major), kh*kw, n-blocks
-    int vec_epi;            // float4 epilogue (channel counts % 4 == 0, 16-byte aligned buffers)
-    int ksplit, t_per;      // split-K: blocks per tile and 16-wide K stages per split
-    float* part;            // split-K partial tiles [ksplit][M][N]
-    const float* resid;     // RESID: NHWC tensor shaped like dst0, added before ReLU / mask
-    int shuf_h, shuf_w, shuf_off;   // SHUFFLE2 output grid and crop offset
-    FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
-    int in_pix;             // batch * Hi * Wi (lean kernel's buffer extent)
-};
 
 // Load 4 consecutive k values (k, k+1, k+2, k+3) of GEMM row (pb, hb, wb) into v.
 template <int MODE>
@@ -86,64 +62,6 @@ __device__ __forceinline__ f32x4 load_a4(const IgemmParams& p, int pb, int hb, i
     }
 }
 
-// Output position of GEMM row m: the pixel itself, or (SHUFFLE2) the batch row base b*shuf_h and
-// the top-left corner (2ho - off, 2wo - off) of its 2x2 output block.
-struct EpiRow {
-    long long pix;
-    int oh0, ow0;
-};
-
-__device__ __forceinline__ EpiRow epi_row(const IgemmParams& p, int m) {
-    if (!(p.flags & PU_EPI_SHUFFLE2)) return {m, 0, 0};
-    const int t2 = fdiv(m, p.dWo);
-    const int wo = m - t2 * p.Wo;
-    const int bb = fdiv(t2, p.dHo);
-    const int ho = t2 - bb * p.Ho;
-    return {(long long)bb * p.shuf_h, 2 * ho - p.shuf_off, 2 * wo - p.shuf_off};
-}
-
-// SHUFFLE2 destination element offset of channel n of row r; false if cropped away
-__device__ __forceinline__ bool shuf_off(const IgemmParams& p, const EpiRow& r, int n, long long* off, int* c) {
-    const int co = p.N >> 2;
-    const int ij = fdiv(n, p.dCo);
-    *c = n - ij * co;
-    const int oh = r.oh0 + (ij >> 1), ow = r.ow0 + (ij & 1);
-    if ((unsigned)oh >= (unsigned)p.shuf_h || (unsigned)ow >= (unsigned)p.shuf_w) return false;
-    *off = ((r.pix + oh) * p.shuf_w + ow) * co + *c;
-    return true;
-}
-
-// float4 epilogue of channels n..n+3 (n % 4 == 0, vec_epi) of row r.
-__device__ __forceinline__ void epi_store4(const IgemmParams& p, const EpiRow& r, int n, f32x4 v) {
-    float* dst;
-    const float* msk;
-    long long off;
-    int nb;   // bias index of the first channel
-    const long long pix = r.pix;
-    if (p.flags & PU_EPI_SHUFFLE2) {
-        if (!shuf_off(p, r, n, &off, &nb)) return;
-        dst = p.dst0; msk = p.mask0;
-    } else if (n < p.n0) {
-        off = pix * p.n0 + n;
-        dst = p.dst0; msk = p.mask0; nb = n;
-    } else {
-        off = pix * (p.N - p.n0) + (n - p.n0);
-        dst = p.dst1; msk = p.mask1; nb = n;
-    }
-    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + nb);
-    if (p.resid) v += *reinterpret_cast<const f32x4*>(p.resid + off);
-    if (p.flags & PU_EPI_RELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    if (msk) {
-        const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
-    }
-    if (p.flags & PU_EPI_ACCUM) v += *reinterpret_cast<const f32x4*>(dst + off);
-    *reinterpret_cast<f32x4*>(dst + off) = v;
-}
 
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m_blk,
@@ -566,7 +484,6 @@ __global__ __launch_bounds__(256) void igemm_dma_kernel(const IgemmParams p) {
 // Weights come pre-split (pu_split_weight6: [k/16][q = plane*2 + half][n][8 bf16]); pixel rows
 // are staged as fp32 exactly like igemm_dma_kernel and split after the LDS read (VALU work that
 // co-issues with the MFMAs).  Same loader, ring, swizzle, epilogue and split-K as the fp32 kernel.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split3_bf16(const f32x4 lo4, const f32x4 hi4, bf16x8_t& h, bf16x8_t& m, bf16x8_t& l) {
 #pragma clang fp contract(off)
@@ -781,36 +698,6 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
 // Requirements (host: lean_ok): 3x3 taps, K order cgroup 16 (CG 1) or 32 (CG 2), c1 == 0 or
 // c1 == c0 (one pixel stride for both sources), K == k_pad, split-K on group boundaries,
 // every tensor under 2 GB.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ unsigned pk_bf16(f32x2 v) {
-    const bf16x2_t h = __builtin_convertvector(v, bf16x2_t);
-    return __builtin_bit_cast(unsigned, h);
-}
-
-// x = hi + mid + lo exactly (round-to-nearest at each step), 8 elements as 4 pairs
-__device__ __forceinline__ void split3_pairs(const f32x4 lo4, const f32x4 hi4, bf16x8_t& h, bf16x8_t& m, bf16x8_t& l) {
-#pragma clang fp contract(off)
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 hv, mv, lv;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const f32x2 x = q < 2 ? f32x2{lo4[2 * q], lo4[2 * q + 1]} : f32x2{hi4[2 * q - 4], hi4[2 * q - 3]};
-        const unsigned a = pk_bf16(x);
-        const f32x2 af = {__builtin_bit_cast(float, a << 16), __builtin_bit_cast(float, a & 0xffff0000u)};
-        const f32x2 r = x - af;
-        const unsigned b = pk_bf16(r);
-        const f32x2 bf = {__builtin_bit_cast(float, b << 16), __builtin_bit_cast(float, b & 0xffff0000u)};
-        const f32x2 c = r - bf;
-        hv[q] = a;
-        mv[q] = b;
-        lv[q] = pk_bf16(c);
-    }
-    h = __builtin_bit_cast(bf16x8_t, hv);
-    m = __builtin_bit_cast(bf16x8_t, mv);
-    l = __builtin_bit_cast(bf16x8_t, lv);
-}
 
 template <int BM, int BN, int WM, int WN, int NW, int CG>
 __global__ __launch_bounds__(NW * 64) void igemm_x6_lean_kernel(const IgemmParams p) {
@@ -1484,6 +1371,17 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
 #undef PU_SC
         return check_launch("pu_conv_igemm (small-channel)");
     }
+    if (wino_ok(a, p.vec_epi)) {
+        PU_REQUIRE(((uintptr_t)a->weight6 & 15) == 0, "pu_conv_igemm: weight6 must be 16-byte aligned");
+        p.gn = N / 64;
+        p.part = (float*)a->workspace;
+        p.ksplit = wino_launch(a, p, s);
+        if (p.ksplit > 1) {
+            const long long tot = M * (N / 4);
+            hipLaunchKernelGGL(igemm_splitk_epilogue_kernel, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s, p);
+        }
+        return check_launch("pu_conv_igemm (winograd x6)");
+    }
     int bm, bn;
     plan_tiles(a, M, &bm, &bn, &p.ksplit, &p.t_per);
     p.gn = ceil_div(N, bn);
@@ -1557,6 +1455,7 @@ extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
     if (!a || a->batch <= 0 || a->out_h <= 0 || a->out_w <= 0 || a->n <= 0 || a->k_pad <= 0) return 0;
     const long long M = (long long)a->batch * a->out_h * a->out_w;
     if (small_conv_ok(a) || stem_conv_ok(a) || conv1x1_small_ok(a)) return 0;
+    if (wino_ok(a, vec_epilogue(a))) return wino_workspace_bytes(a);
     int bm, bn, ks, tp;
     plan_tiles(a, M, &bm, &bn, &ks, &tp);
     return split_bytes(M, a->n, ks);
@@ -1588,6 +1487,16 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         *bn = a->n;
         *mode = 3;
         if (ksplit) *ksplit = 1;
+        return PU_OK;
+    }
+    if (wino_ok(a, vec_epilogue(a))) {  // reported as mode 6 ("wino"), 64 tiles (256 pixels) x 64 channels
+        *bm = 256;
+        *bn = 64;
+        *mode = 6;
+        if (ksplit) {
+            const size_t need = wino_workspace_bytes(a);
+            *ksplit = need && a->workspace && a->ws_bytes >= need ? (int)(need / ((size_t)M * a->n * 4)) : 1;
+        }
         return PU_OK;
     }
     if (ksplit) *ksplit = (ks > 1 && a->workspace && a->ws_bytes >= split_bytes(M, a->n, ks)) ? ks : 1;

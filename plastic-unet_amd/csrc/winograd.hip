@@ -1,0 +1,494 @@
+// Winograd F(2x2, 3x3) convolution for the fp32 3x3/s1/p1 layers, on the exact 6-product bf16
+// MFMA scheme of igemm.hip (each fp32 product as hi/mid/lo bf16 terms, fp32 accumulation).
+//
+// Replaces (yaricom/Plastic-UNet): the nn.Conv2d(k=3, p=1) of double_conv (src/unet/unet_p.py:
+// 184-201) forward and backward-data, over the skip concat torch.cat([x2, x1], 1) (unet_p.py:248)
+// without materialising it - the same layers igemm_x6_lean_kernel computes directly.
+//
+// Arithmetic (Lavin & Gray's F(2x2,3x3)): a 2x2 output tile y of one (image, channel n) is
+//   y = A^T [ sum_c (G g_nc G^T) (.) (B^T d_c B) ] A
+// with d_c the 4x4 input window of channel c, g_nc the 3x3 kernel, (.) the element-wise product
+// over the 16 positions xi = (i, j), and
+//   B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1],  G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1],
+//   A^T = [1 1 1 0; 0 1 -1 -1].
+// So each xi is an independent GEMM  M_xi[n][tile] = sum_c U_xi[n][c] V_xi[c][tile]  with K = C
+// instead of 9C: 16 products per 4 outputs instead of 36 (2.25x fewer MFMAs).  U = G g G^T is
+// formed in fp64 once per weight update (pu_pack_wino) and rounded to fp32; V = B^T d B and the
+// output transform are fp32 adds/subtracts (no multiplications: the transforms only scale by +-1).
+// The numerics are fp32 arithmetic throughout (tests/test_precision_gpu.py bounds vs fp64).
+//
+// Kernel (one block = 64 tiles x 64 output channels, 4 waves as 2 x 2, each wave a 32 x 32 MFMA
+// tile for all 16 xi: 16 accumulators of 16 fp32 = 256 AGPRs, one wave per SIMD):
+//   * a 16-channel chunk is split into 4 sub-stages, one per row i of B^T (xi = 4i .. 4i+3);
+//   * a sub-stage's LDS slot holds V_xi (4 xi x 3 planes x 64 tiles x 16 channels, bf16) and
+//     U_xi (4 xi x 3 planes x 64 channels x 16), 24 KB each; 2 slots, one barrier per sub-stage;
+//   * thread (tile tt, channel quad q) keeps the 4x4 window of its 4 channels in registers (16
+//     buffer_load_dwordx4, out-of-image pixels fall outside the buffer range and read 0), two
+//     chunks in flight (two register banks), and during sub-stage s forms V of sub-stage s+1 -
+//     8 adds and one exact 3-term split per (xi row, 4 channels) - while the MFMAs of s run;
+//   * U comes pre-split from HBM/L2 by buffer_load ... lds (6 x 1 KB pieces per wave per
+//     sub-stage); 32-byte LDS rows with the 16-byte halves swapped on rows 8..15 mod 16 make
+//     every ds_read_b128 operand read and ds_write_b64 V store conflict-free;
+//   * epilogue: the output transform is lane-local (a lane holds all 16 xi of the same (tile,
+//     4 channels)), then igemm's float4 epilogue (bias, ReLU, residual, masks, concat split,
+//     accumulate) per output pixel; split-K writes pre-bias partial tiles for
+//     igemm_splitk_epilogue_kernel.
+#include "conv_common.h"
+
+namespace pu {
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int WG_BM = 64;                      // tiles per block
+constexpr int WG_BN = 64;                      // output channels per block
+constexpr int WG_HALF = 4 * 3 * 64 * 32;       // bytes of V (or U) in one sub-stage slot
+constexpr int WG_SLOT = 2 * WG_HALF;
+
+struct WinoParams {
+    IgemmParams p;        // grid (Ho == Hi, Wo == Wi), sources, epilogue, split-K partials
+    const __bf16* U;      // [C/16][16 xi][3 planes][N][16] (pu_pack_wino)
+    int tiles;            // batch * Ho/2 * Wo/2
+    int kc_per;           // 16-channel chunks per K split (even)
+    int gm;               // tile blocks
+    FastDiv dTw, dTh;     // tile index -> (image, tile row, tile column)
+    unsigned a_bytes;     // extent of the shifted pixel buffers
+    unsigned u_bytes;     // extent of U
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
+#pragma clang fp contract(off)
+    const IgemmParams& p = w.p;
+    // two sub-stage slots, each V (VALU-stored) and U (LDS-DMA) as separate arrays: the compiler
+    // then knows the V stores / operand reads do not alias the DMA in flight (no vmcnt(0) before
+    // every LDS access)
+    __shared__ __attribute__((aligned(16))) unsigned char ldv0[WG_HALF];
+    __shared__ __attribute__((aligned(16))) unsigned char ldv1[WG_HALF];
+    __shared__ __attribute__((aligned(16))) unsigned char ldu0[WG_HALF];
+    __shared__ __attribute__((aligned(16))) unsigned char ldu1[WG_HALF];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave & 1, wn = (wave >> 1) & 1, wx = wave >> 2;
+
+    int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int per_split = w.gm * p.gn;
+    const int kz = blk / per_split;
+    blk -= kz * per_split;
+    const int mb = blk / p.gn;
+    const int m_blk = mb * WG_BM;
+    const int n_blk = (blk - mb * p.gn) * WG_BN;
+    const int kc0 = kz * w.kc_per;
+    const int kc1 = min(p.C / 16, kc0 + w.kc_per);
+
+    // ---- producer role: tile tt of the block, channels 2q, 2q+1 of each 16-channel chunk.
+    // Window pixel (r, s) of the tile is row offset vrow[r] (or out of range) + s pixels; only
+    // rows 0 / 3 and columns 0 / 3 can leave the image.
+    const int tt = tid >> 3, q = tid & 7;
+    const int cs = p.c0;                       // pixel stride (== c1 when c1 != 0)
+    const int shift = p.Wi + 1;                // window corner (2ty-1, 2tx-1) >= (-1, -1)
+    unsigned vrow[4];
+    bool col0_ok = false, col3_ok = false;
+    {
+        const int m = m_blk + tt;
+        int ty = 0, tx = 0, b = 0;
+        const bool mv = m < w.tiles;
+        if (mv) {
+            const int t2 = fdiv(m, w.dTw);
+            tx = m - t2 * (p.Wo >> 1);
+            b = fdiv(t2, w.dTh);
+            ty = t2 - b * (p.Ho >> 1);
+        }
+        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + q * 8);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
+        col0_ok = x0 >= 0;
+        col3_ok = x0 + 3 < p.Wi;
+    }
+    const unsigned pixb = (unsigned)cs * 4u;
+    const float* a0 = p.src0 - (long long)shift * cs;
+    const float* a1 = (p.c1 ? p.src1 : p.src0) - (long long)shift * cs;
+    // V store address of this thread inside a slot (row tt, its 4-byte pair, swizzled half)
+    const int v_st = tt * 32 + (((q >> 2) ^ ((tt >> 3) & 1)) * 16) + (q & 3) * 4;
+
+    // ---- U loader: wave w fills pieces 3w .. 3w+2 (piece P = (j*3 + plane)*2 + row half)
+    const unsigned u_lane = (unsigned)((lane >> 1) * 32 + (((lane & 1) ^ ((lane >> 4) & 1)) * 16));
+    const unsigned u_row = (unsigned)p.N * 32u;                  // bytes per (xi, plane) block
+
+    // ---- MFMA role: positions j = 2wx, 2wx+1 of every row i; operand rows 32*wn + (lane&31)
+    // of U and 32*wm + (lane&31) of V
+    const int rd_sw = (((lane >> 5) ^ ((lane >> 3) & 1)) * 16);
+    const int u_rd = (32 * wn + (lane & 31)) * 32 + rd_sw + 2 * wx * 3 * 2048;
+    const int v_rd = (32 * wm + (lane & 31)) * 32 + rd_sw + 2 * wx * 3 * 2048;
+
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+    f32x2v d[16];
+    f32x16 acc[8];                            // [i][jj]
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+
+    // the 4x4 window of chunk kc (a chunk past the split's end reads zeros: empty buffer range)
+    auto load_d = [&](int kc) {
+        const int c = kc * 16;
+        const bool second = c >= p.c0;
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, kc < kc1 ? w.a_bytes : 0u);
+        const unsigned cb = (unsigned)((second ? c - p.c0 : c) * 4);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int rr = e >> 2, ss = e & 3;
+            unsigned vo = vrow[rr];
+            if (ss == 0) vo = col0_ok ? vo : LEAN_OOB;
+            if (ss == 3) vo = col3_ok ? vo : LEAN_OOB;
+            const unsigned soff = __builtin_amdgcn_readfirstlane(cb + ss * pixb);
+            d[e] = __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0));
+        }
+    };
+    // U pieces of sub-stage (chunk kc, row i) into slot base sb
+    auto load_u = [&](int kc, int i, unsigned char* base) {
+        const unsigned bytes = kc < kc1 ? w.u_bytes : 0u;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+            const int P = wave * 3 + e;
+            const int jp = P >> 1, half = P & 1;
+            const int j = jp / 3, pl = jp - 3 * (jp / 3);
+            const unsigned soff = (unsigned)(((kc * 16 + 4 * i + j) * 3 + pl)) * u_row + (unsigned)(n_blk * 32 + half * 1024);
+            lean_load(w.U, bytes, base + P * 1024, u_lane, soff);
+        }
+    };
+    // V = row i of B^T d B for this thread's 2 channels -> hi/mid/lo planes in V array sb
+    auto make_v = [&](auto i_c, unsigned char* sb) {
+        constexpr int i = decltype(i_c)::value;
+        f32x2v t[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            if constexpr (i == 0) t[s2] = d[s2] - d[8 + s2];
+            else if constexpr (i == 1) t[s2] = d[4 + s2] + d[8 + s2];
+            else if constexpr (i == 2) t[s2] = d[8 + s2] - d[4 + s2];
+            else t[s2] = d[4 + s2] - d[12 + s2];
+        }
+        const f32x2v v0 = t[0] - t[2], v1 = t[1] + t[2], v2 = t[2] - t[1], v3 = t[1] - t[3];
+        bf16x8_t h, m, l;
+        split3_pairs(f32x4{v0[0], v0[1], v1[0], v1[1]}, f32x4{v2[0], v2[1], v3[0], v3[1]}, h, m, l);
+        const u32x4 pv[3] = {__builtin_bit_cast(u32x4, h), __builtin_bit_cast(u32x4, m), __builtin_bit_cast(u32x4, l)};
+        unsigned char* base = sb + v_st;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(base + (j * 3 + pl) * 2048) = pv[pl][j];
+    };
+    // the 6 MFMAs of position (i, 2wx + jj) from the V / U arrays sv / su
+    auto mma = [&](auto x_c, const unsigned char* sv, const unsigned char* su, int jj) {
+        constexpr int x = decltype(x_c)::value;
+        const unsigned char* ub = su + u_rd + jj * 3 * 2048;
+        const unsigned char* vb = sv + v_rd + jj * 3 * 2048;
+        bf16x8_t fu[3], fv[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            fu[pl] = *reinterpret_cast<const bf16x8_t*>(ub + pl * 2048);
+            fv[pl] = *reinterpret_cast<const bf16x8_t*>(vb + pl * 2048);
+        }
+        f32x16 c = acc[x];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[1], fv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[2], fv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[0], fv[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[1], fv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[0], fv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[0], fv[0], c, 0, 0, 0);
+        acc[x] = c;
+    };
+    using I0 = std::integral_constant<int, 0>;
+
+    // prologue: chunk kc0's window, sub-stage (kc0, 0) in slot 0
+    load_d(kc0);
+    load_u(kc0, 0, ldu0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    make_v(I0{}, ldv0);
+
+    // one sub-stage (kc, i) in slot i & 1: wait for its U pieces and every wave's V stores;
+    // issue the next sub-stage's U; form the next sub-stage's V (into the other slot - a
+    // separate LDS array, so the compiler sees it independent of the operand reads) between
+    // this sub-stage's two MFMA groups.  The window of chunk kc+1 is loaded into the same
+    // registers once row 3 of chunk kc is formed (sub-stage 2) and waited for in sub-stage 3
+    // behind the first MFMA group.
+    auto sub = [&](int kc, auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        unsigned char* cv = (i & 1) ? ldv1 : ldv0;
+        unsigned char* cu = (i & 1) ? ldu1 : ldu0;
+        unsigned char* nv = (i & 1) ? ldv0 : ldv1;
+        unsigned char* nu = (i & 1) ? ldu0 : ldu1;
+        if constexpr (i == 3) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if constexpr (i < 3) {
+            load_u(kc, i + 1, nu);
+            mma(std::integral_constant<int, 2 * i>{}, cv, cu, 0);
+            make_v(std::integral_constant<int, i + 1>{}, nv);
+            if constexpr (i == 2) load_d(kc + 1);
+            mma(std::integral_constant<int, 2 * i + 1>{}, cv, cu, 1);
+        } else {
+            load_u(kc + 1, 0, nu);
+            mma(std::integral_constant<int, 6>{}, cv, cu, 0);
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            make_v(I0{}, nv);
+            mma(std::integral_constant<int, 7>{}, cv, cu, 1);
+        }
+    };
+
+    for (int kc = kc0; kc < kc1; ++kc) {
+        sub(kc, std::integral_constant<int, 0>{});
+        sub(kc, std::integral_constant<int, 1>{});
+        sub(kc, std::integral_constant<int, 2>{});
+        sub(kc, std::integral_constant<int, 3>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // ---- output transform Y = A^T M A.  Wave wx holds positions j = 2wx, 2wx+1 of every row i
+    // for its (32 tiles x 32 channels); per element s_py[j] = sum_i A^T[py][i] M[i][j].  Wave wx
+    // finishes output row py = wx of the tile: Y[py][0] = (s[0] + s[1]) + s[2],
+    // Y[py][1] = s[1] - (s[2] + s[3]); the partner wave (same wm, wn) supplies the other half.
+    // exchange buffers: wx = 0 writes V slot 0 + U slot 0, wx = 1 the slot-1 pair; per (wm, wn)
+    // [2][16][64] floats (8 KB): two of them per 24 KB array
+    unsigned char* xw = (wm ? (wx ? ldu1 : ldu0) : (wx ? ldv1 : ldv0)) + wn * 8192;
+    const unsigned char* xq = (wm ? (wx ? ldu0 : ldu1) : (wx ? ldv0 : ldv1)) + wn * 8192;
+    float* xs = reinterpret_cast<float*>(xw);
+    const float* xr = reinterpret_cast<const float*>(xq);
+    float own0[16], own1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float sp[2][2];                                  // [py][jj]
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            sp[0][jj] = acc[0 * 2 + jj][r] + acc[1 * 2 + jj][r] + acc[2 * 2 + jj][r];
+            sp[1][jj] = acc[1 * 2 + jj][r] - acc[2 * 2 + jj][r] - acc[3 * 2 + jj][r];
+        }
+        // wx = 0 (j = 0, 1): keeps row 0, sends row 1 as (s0 + s1, s1);
+        // wx = 1 (j = 2, 3): keeps row 1, sends row 0 as (s2, s2 + s3)
+        const int keep = wx, send = 1 - wx;
+        const float k0 = wx == 0 ? sp[keep][0] + sp[keep][1] : sp[keep][0];
+        const float k1 = wx == 0 ? sp[keep][1] : sp[keep][0] + sp[keep][1];
+        const float s0v = wx == 0 ? sp[send][0] + sp[send][1] : sp[send][0];
+        const float s1v = wx == 0 ? sp[send][1] : sp[send][0] + sp[send][1];
+        xs[(0 * 16 + r) * 64 + lane] = s0v;
+        xs[(1 * 16 + r) * 64 + lane] = s1v;
+        own0[r] = k0;
+        own1[r] = k1;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int m = m_blk + 32 * wm + (lane & 31);
+    if (m >= w.tiles) return;
+    const int t2 = fdiv(m, w.dTw);
+    const int tx = m - t2 * (p.Wo >> 1);
+    const int b = fdiv(t2, w.dTh);
+    const int ty = t2 - b * (p.Ho >> 1);
+    const long long pix0 = ((long long)b * p.Ho + 2 * ty + wx) * p.Wo + 2 * tx;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int n = n_blk + 32 * wn + 8 * g + 4 * (lane >> 5);
+        f32x4 y0, y1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g + e;
+            const float o0 = xr[(0 * 16 + r) * 64 + lane];
+            const float o1 = xr[(1 * 16 + r) * 64 + lane];
+            // wx = 0: own = (s0 + s1, s1), other = (s2, s2 + s3);  wx = 1: own = (s2, s2 + s3)
+            y0[e] = wx == 0 ? own0[r] + o0 : o0 + own0[r];
+            y1[e] = wx == 0 ? own1[r] - o1 : o1 - own1[r];
+        }
+        if (p.ksplit == 1) {
+            epi_store4(p, EpiRow{pix0, 0, 0}, n, y0);
+            epi_store4(p, EpiRow{pix0 + 1, 0, 0}, n, y1);
+        } else {
+            float* part = p.part + (long long)kz * p.M * p.N;
+            *reinterpret_cast<f32x4*>(part + pix0 * p.N + n) = y0;
+            *reinterpret_cast<f32x4*>(part + (pix0 + 1) * p.N + n) = y1;
+        }
+    }
+}
+
+// U = G g G^T per (n, 8 consecutive c), fp64 then rounded to fp32 and split into hi/mid/lo bf16:
+// out[((c/16*16 + xi)*3 + plane)*N + n][c % 16].  Forward: g = w[n][c]; dgrad (the transposed,
+// flipped kernel of the data gradient): output channel n = input channel of w, c = its output
+// channel, g[r][s] = w[c][n][2-r][2-s].
+struct WinoPackJob {
+    const float* w;
+    __bf16* out;
+    int n, c, dgrad, blocks;
+};
+constexpr int WINO_MAX_JOBS = 64;
+struct WinoPackBatch {
+    WinoPackJob job[WINO_MAX_JOBS];
+    int count;
+};
+
+__global__ __launch_bounds__(256) void wino_pack_kernel(const WinoPackBatch bt) {
+#pragma clang fp contract(off)
+    int j = 0, b0 = 0;
+    while (j + 1 < bt.count && (int)blockIdx.x >= b0 + bt.job[j].blocks) b0 += bt.job[j++].blocks;
+    const WinoPackJob J = bt.job[j];
+    const int idx = ((int)blockIdx.x - b0) * 256 + threadIdx.x;   // (c8 group, n): n fastest
+    const int c8s = J.c / 8;
+    if (idx >= J.n * c8s) return;
+    const int n = idx % J.n;
+    const int c8 = idx / J.n;
+    typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+    const int chunk = c8 >> 1, half = c8 & 1;
+    // one row a of G g G^T at a time (12 output vectors live instead of 48)
+#pragma unroll 1
+    for (int a = 0; a < 4; ++a) {
+        bf16x8v o[4][3];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int c = c8 * 8 + e;
+            double g[3][3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+                    g[r][s] = J.dgrad ? (double)J.w[(((long long)c * J.n + n) * 3 + (2 - r)) * 3 + (2 - s)]
+                                      : (double)J.w[(((long long)n * J.c + c) * 3 + r) * 3 + s];
+            double t[3];   // row a of G g
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+                t[s] = a == 0 ? g[0][s] : a == 1 ? 0.5 * (g[0][s] + g[1][s] + g[2][s])
+                     : a == 2 ? 0.5 * (g[0][s] - g[1][s] + g[2][s]) : g[2][s];
+            const double u[4] = {t[0], 0.5 * (t[0] + t[1] + t[2]), 0.5 * (t[0] - t[1] + t[2]), t[2]};
+#pragma unroll
+            for (int bc = 0; bc < 4; ++bc) {
+                const float x = (float)u[bc];
+                const __bf16 h = (__bf16)x;
+                const float rr = x - (float)h;
+                const __bf16 mm = (__bf16)rr;
+                o[bc][0][e] = h;
+                o[bc][1][e] = mm;
+                o[bc][2][e] = (__bf16)(rr - (float)mm);
+            }
+        }
+#pragma unroll
+        for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                *reinterpret_cast<bf16x8v*>(J.out + ((((long long)chunk * 16 + a * 4 + bc) * 3 + pl) * J.n + n) * 16 + half * 8) = o[bc][pl];
+    }
+}
+
+// host side -------------------------------------------------------------------------------------
+
+// the layers the Winograd kernel takes (the caller passed U): 3x3 / s1 / p1, same-size even grid,
+// 16-channel chunks from one source each with one pixel stride (c1 == 0 or c1 == c0), an even
+// number of chunks, 64-channel output blocks, the float4 epilogue, no ConvT shuffle, buffers
+// addressable with 32-bit offsets
+bool wino_ok(const pu_conv_args* a, bool vec_epi) {
+    const int C = a->c0 + a->c1;
+    if (!a->wino || !a->weight6) return false;
+    if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1) return false;
+    if (a->in_h != a->out_h || a->in_w != a->out_w || (a->out_h & 1) || (a->out_w & 1)) return false;
+    if (a->c0 % 16 || (a->c1 != 0 && a->c1 != a->c0) || C % 32) return false;
+    if (a->n % WG_BN || !vec_epi || (a->flags & PU_EPI_SHUFFLE2)) return false;
+    const long long px = (long long)a->batch * a->in_h * a->in_w + a->in_w + 1;
+    if (px * a->c0 * 4 >= (1LL << 31)) return false;
+    if ((long long)C * a->n * 96 >= (1LL << 31)) return false;
+    return ((uintptr_t)a->wino & 15) == 0;
+}
+
+// K split so that small tile grids (8x8 / 16x16 levels) still give ~1 block per CU: even chunk
+// counts per split, >= 8 chunks (128 channels) each
+void wino_plan(const pu_conv_args* a, int* ksplit, int* kc_per) {
+    const int C = a->c0 + a->c1;
+    const long long tiles = (long long)a->batch * (a->out_h / 2) * (a->out_w / 2);
+    const int blocks = ceil_div(tiles, WG_BM) * (a->n / WG_BN);
+    const int chunks = C / 16;
+    *ksplit = 1;
+    *kc_per = chunks;
+    if (blocks >= 240) return;
+    int ks = ceil_div(256, blocks);
+    if (ks > chunks / 8) ks = chunks / 8;
+    if (ks < 2) return;
+    int per = ceil_div(chunks, ks);
+    per += per & 1;
+    *kc_per = per;
+    *ksplit = ceil_div(chunks, per);
+}
+
+int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
+    WinoParams w;
+    w.p = p;
+    w.U = reinterpret_cast<const __bf16*>(a->wino);
+    w.tiles = a->batch * (a->out_h / 2) * (a->out_w / 2);
+    w.gm = ceil_div(w.tiles, WG_BM);
+    w.p.gn = a->n / WG_BN;
+    w.dTw = make_fastdiv(a->out_w / 2);
+    w.dTh = make_fastdiv(a->out_h / 2);
+    w.a_bytes = (unsigned)(((long long)a->batch * a->in_h * a->in_w + a->in_w + 1) * a->c0 * 4);
+    w.u_bytes = (unsigned)((long long)(a->c0 + a->c1) * a->n * 96);
+    int ks, per;
+    wino_plan(a, &ks, &per);
+    if (ks > 1 && (!a->workspace || a->ws_bytes < (size_t)ks * p.M * p.N * sizeof(float))) {
+        ks = 1;
+        per = (a->c0 + a->c1) / 16;
+    }
+    w.p.ksplit = ks;
+    w.p.part = (float*)a->workspace;
+    w.kc_per = per;
+    hipLaunchKernelGGL(wino_x6_kernel, dim3((unsigned)(w.gm * w.p.gn * ks)), dim3(512), 0, s, w);
+    return ks;
+}
+
+size_t wino_workspace_bytes(const pu_conv_args* a) {
+    int ks, per;
+    wino_plan(a, &ks, &per);
+    return ks > 1 ? (size_t)ks * a->batch * a->out_h * a->out_w * a->n * sizeof(float) : 0;
+}
+
+}  // namespace pu
+
+using namespace pu;
+
+extern "C" size_t pu_wino_bytes(int n, int c) {
+    return (n > 0 && c > 0 && c % 16 == 0) ? (size_t)n * c * 96 : 0;
+}
+
+extern "C" int pu_pack_wino(const pu_wino_job* jobs, int n_jobs, void* stream) {
+    PU_REQUIRE(n_jobs >= 0 && (n_jobs == 0 || jobs), "pu_pack_wino: bad job list");
+    for (int i0 = 0; i0 < n_jobs; i0 += WINO_MAX_JOBS) {
+        WinoPackBatch b;
+        b.count = 0;
+        int total = 0;
+        for (int i = i0; i < n_jobs && i < i0 + WINO_MAX_JOBS; ++i) {
+            const pu_wino_job& J = jobs[i];
+            PU_REQUIRE(J.w && J.out && J.cout > 0 && J.cin > 0, "pu_pack_wino: job %d incomplete", i);
+            const int n = J.dgrad ? J.cin : J.cout, c = J.dgrad ? J.cout : J.cin;
+            PU_REQUIRE(c % 16 == 0, "pu_pack_wino: job %d reduces over %d channels (need a multiple of 16)", i, c);
+            PU_REQUIRE(((uintptr_t)J.out & 15) == 0, "pu_pack_wino: job %d output must be 16-byte aligned", i);
+            WinoPackJob& o = b.job[b.count++];
+            o.w = J.w;
+            o.out = (__bf16*)J.out;
+            o.n = n;
+            o.c = c;
+            o.dgrad = J.dgrad != 0;
+            o.blocks = ceil_div((long long)n * (c / 8), 256);
+            total += o.blocks;
+        }
+        hipLaunchKernelGGL(wino_pack_kernel, dim3((unsigned)total), dim3(256), 0, as_stream(stream), b);
+        const int st = check_launch("pu_pack_wino");
+        if (st != PU_OK) return st;
+    }
+    return PU_OK;
+}

@@ -22,6 +22,9 @@ PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD, PU
 PU_RULE_HEBB, PU_RULE_OJA = 0, 1
 
 
+ABI_VERSION = 2    # include/plastic_unet.h PU_ABI_VERSION
+
+
 class ConvArgs(ctypes.Structure):
     _fields_ = [("batch", c_int), ("in_h", c_int), ("in_w", c_int), ("out_h", c_int), ("out_w", c_int),
                 ("kh", c_int), ("kw", c_int), ("stride", c_int), ("pad", c_int),
@@ -30,7 +33,7 @@ class ConvArgs(ctypes.Structure):
                 ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int),
                 ("workspace", P), ("ws_bytes", c_size),
                 ("resid", P), ("shuf_h", c_int), ("shuf_w", c_int), ("shuf_off", c_int),
-                ("weight6", P)]
+                ("weight6", P), ("wino", P)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -61,6 +64,10 @@ class AdamTensor(ctypes.Structure):
     _fields_ = [("param", P), ("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("numel", c_ll)]
 
 
+class WinoJob(ctypes.Structure):
+    _fields_ = [("w", P), ("out", P), ("cout", c_int), ("cin", c_int), ("dgrad", c_int)]
+
+
 class PackJob(ctypes.Structure):
     _fields_ = [("w", P), ("packed", P), ("packed_bf16", P), ("planes", P), ("mode", c_int), ("d0", c_int),
                 ("d1", c_int), ("kh", c_int), ("kw", c_int), ("k_pad", c_int), ("cgroup", c_int)]
@@ -83,6 +90,8 @@ SIGNATURES = [
                               ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     ("pu_pack_weight", c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_split_weight6", c_int, [P, P, c_int, c_int, P]),
+    ("pu_wino_bytes", c_size, [c_int, c_int]),
+    ("pu_pack_wino", c_int, [ctypes.POINTER(WinoJob), c_int, P]),
     ("pu_nchw_to_nhwc", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_channel_scale", c_int, [P, P, P, c_int, c_ll, c_int, P]),
     ("pu_conv_igemm_bf16", c_int, [ctypes.POINTER(ConvArgs), P]),
@@ -150,8 +159,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.pu_abi_version() != 1:
-        raise LibraryMissing("libplastic_unet.so ABI %d != 1" % lib.pu_abi_version())
+    if lib.pu_abi_version() != ABI_VERSION:
+        raise LibraryMissing("libplastic_unet.so ABI %d != %d" % (lib.pu_abi_version(), ABI_VERSION))
     _lib = lib
     return lib
 

@@ -9,7 +9,7 @@ import os
 import torch
 
 from . import _lib
-from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, check,
+from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, WinoJob, check,
                    PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
@@ -23,7 +23,7 @@ def lib():
 
 # ------------------------------------------------------------------------------ launch profiler
 _PROF = None
-_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem"}
+_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem", 6: "wino"}
 
 # fp32 GEMM arithmetic of the MFMA convolutions: "split6" (default) = each fp32 product as 6 exact
 # bf16 products on the bf16 MFMA pipe (pu_split_weight6 / pu_conv_args.weight6, fp32-accurate);
@@ -51,6 +51,44 @@ def _halo_flags():
 
 def fp32_math():
     return _FP32_MATH
+
+
+# fp32 3x3/s1/p1 convolutions (forward and data gradient) on the Winograd F(2x2,3x3) kernel where
+# the layer qualifies (PU_WINO=0: the direct 6-product kernels everywhere; A/B runs, tests flip it
+# with set_wino)
+_WINO = os.environ.get("PU_WINO", "1") != "0"
+
+
+def set_wino(on):
+    """Route eligible fp32 3x3 convolutions to the Winograd kernel (True) or the direct kernels.
+    Returns the previous setting."""
+    global _WINO
+    prev, _WINO = _WINO, bool(on)
+    return prev
+
+
+def wino_wanted(w, mode):
+    """Whether a packed conv operand of parameter w (OIHW 3x3) should carry a Winograd operand:
+    the reduced channel count a multiple of 32 and the produced one of 64 (the kernel's chunks
+    and output blocks)."""
+    if mode not in (0, 1) or w.dim() != 4 or w.shape[2:] != (3, 3) or _FP32_MATH != "split6":
+        return False
+    n, c = (w.shape[0], w.shape[1]) if mode == 0 else (w.shape[1], w.shape[0])
+    return c % 32 == 0 and n % 64 == 0
+
+
+def pack_wino(jobs):
+    """pu_pack_wino: jobs = [(w, out, dgrad)] - U = G g G^T of each OIHW weight, exact bf16 planes."""
+    if not jobs:
+        return
+    arr = (WinoJob * len(jobs))()
+    nbytes = 0.0
+    for i, (w, out, dgrad) in enumerate(jobs):
+        _req(w, "w")
+        arr[i] = WinoJob(w.data_ptr(), out.data_ptr(), w.shape[0], w.shape[1], int(dgrad))
+        nbytes += 4.0 * w.numel() + 2.0 * out.numel()
+    with _Rec("pack_wino", nbytes=nbytes):
+        check(lib().pu_pack_wino(arr, len(jobs), _stream()), "pu_pack_wino")
 
 
 def set_fp32_math(mode):
@@ -179,6 +217,9 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
     w6 = getattr(weight, "_split6", None) if (dt != BF16 and _FP32_MATH == "split6") else None
     if w6 is not None:
         a.weight6 = w6.data_ptr()
+        wn = getattr(weight, "_wino", None) if _WINO else None
+        if wn is not None:
+            a.wino = wn.data_ptr()
     L = lib()
     if dt == BF16:
         _igemm_bf16(L, a, batch, out_hw, k, c0, c1, n, dst0)
@@ -287,6 +328,10 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
         check(fn(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, cgroup, _stream()), "pu_pack_weight")
     if out.dtype == torch.float32 and _FP32_MATH == "split6" and k_pad % 16 == 0:
         out._split6 = split_weight6(out)      # travels with the packed operand (igemm picks it up)
+        if wino_wanted(w, mode):              # so does the Winograd operand of a 3x3 conv
+            n, c = (d0, d1) if mode == 0 else (d1, d0)
+            out._wino = torch.empty(lib().pu_wino_bytes(n, c) // 2, dtype=BF16, device=w.device)
+            pack_wino([(w, out._wino, mode == 1)])
     out._pack_spec = (mode, k_pad, cgroup)    # pack_weights() refreshes it in place
     return out
 
@@ -309,6 +354,8 @@ def pack_weights(jobs):
         nbytes += 4.0 * w.numel() + packed.element_size() * packed.numel() + (0 if planes is None else 2.0 * planes.numel())
     with _Rec("pack_weight", nbytes=nbytes):
         check(lib().pu_pack_weights(arr, len(jobs), _stream()), "pu_pack_weights")
+    pack_wino([(w, packed._wino, packed._pack_spec[0] == 1) for w, packed, _ in jobs
+               if getattr(packed, "_wino", None) is not None])
 
 
 def split_weight6(packed):

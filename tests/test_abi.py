@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert set(names) == bound, set(names) ^ bound
     for n in names:
         assert getattr(lib, n) is not None
-    assert lib.pu_abi_version() == 1
+    assert lib.pu_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_invalid_arguments_return_errors_without_gpu():
@@ -75,7 +75,8 @@ def test_header_structs_match_ctypes_layout():
     for cname, py in [("pu_conv_args", _lib.ConvArgs), ("pu_wgrad_args", _lib.WgradArgs),
                       ("pu_plastic_args", _lib.PlasticArgs), ("pu_plastic_bwd_args", _lib.PlasticBwdArgs),
                       ("pu_plastic_head_args", _lib.PlasticHeadArgs),
-                      ("pu_adam_tensor", _lib.AdamTensor), ("pu_pack_job", _lib.PackJob)]:
+                      ("pu_adam_tensor", _lib.AdamTensor), ("pu_pack_job", _lib.PackJob),
+                      ("pu_wino_job", _lib.WinoJob)]:
         body = dict((n, b) for b, n in re.findall(r"typedef struct \{([^}]*)\}\s*(\w+);", src))[cname]
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = []
@@ -131,3 +132,31 @@ def test_trunk_parameter_order_covers_every_trunk_parameter():
         head = {id(m.w), id(m.alpha), id(m.eta)}
         assert trunk | head == {id(p) for p in m.parameters()}
         assert len(t.params) == 4 * depth + 6 * (depth - 1) + 2
+
+
+def test_wino_plan_reported_and_split_k():
+    """pu_conv_igemm_tile reports mode 6 for a Winograd layer, and the 8x8 level splits K."""
+    from punet import _lib
+    L = _lib.load()
+    A = 0x10000
+
+    def args(B, H, c, n, wino, ws=None, ws_bytes=0):
+        a = _lib.ConvArgs(B, H, H, H, H, 3, 3, 1, 1, A, c, None, 0, A, 9 * c, 32, n, A, A, n, None, None, None, 1,
+                          ws, ws_bytes)
+        a.weight6 = A
+        a.wino = A if wino else None
+        return a
+    bm, bn, mode, ks = (ctypes.c_int() for _ in range(4))
+    top = args(32, 128, 64, 64, True)
+    L.pu_conv_igemm_tile(ctypes.byref(top), *(ctypes.byref(v) for v in (bm, bn, mode, ks)))
+    assert (mode.value, ks.value) == (6, 1)
+    assert L.pu_conv_igemm_workspace_bytes(ctypes.byref(top)) == 0
+    bottom = args(32, 8, 1024, 1024, True)
+    nbytes = L.pu_conv_igemm_workspace_bytes(ctypes.byref(bottom))
+    assert nbytes > 0
+    bottom = args(32, 8, 1024, 1024, True, 0x20000, nbytes)
+    L.pu_conv_igemm_tile(ctypes.byref(bottom), *(ctypes.byref(v) for v in (bm, bn, mode, ks)))
+    assert mode.value == 6 and ks.value >= 2
+    direct = args(32, 128, 64, 64, False)
+    L.pu_conv_igemm_tile(ctypes.byref(direct), *(ctypes.byref(v) for v in (bm, bn, mode, ks)))
+    assert mode.value == 4
