@@ -64,6 +64,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// PERSIST: one block per CU walks work items (tile block, channel block, K split); each XCD takes a
+// contiguous range of items (neighbouring tiles share input windows in that XCD's L2) and the
+// next item's first window and U pieces are in flight while the current item's epilogue runs.
+// Otherwise one item per block (XCD-aware order).
+template <bool PERSIST>
 __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 #pragma clang fp contract(off)
     const IgemmParams& p = w.p;
@@ -79,16 +84,23 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave & 1, wn = (wave >> 1) & 1, wx = wave >> 2;
-
-    int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int per_split = w.gm * p.gn;
-    const int kz = blk / per_split;
-    blk -= kz * per_split;
-    const int mb = blk / p.gn;
-    const int m_blk = mb * WG_BM;
-    const int n_blk = (blk - mb * p.gn) * WG_BN;
-    const int kc0 = kz * w.kc_per;
-    const int kc1 = min(p.C / 16, kc0 + w.kc_per);
+    const int total = per_split * p.ksplit;
+
+    // work items of this block: [it, end) with stride step
+    int it, end, step;
+    if (PERSIST) {
+        const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+        const int q8 = total >> 3, r8 = total & 7;
+        const int start = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+        end = start + q8 + (xcd < r8 ? 1 : 0);
+        it = start + local;
+        step = (int)(gridDim.x >> 3);
+    } else {
+        it = xcd_remap(blockIdx.x, gridDim.x);
+        end = it + 1;
+        step = 1;
+    }
 
     // ---- producer role: tile tt of the block, channels 2q, 2q+1 of each 16-channel chunk.
     // Window pixel (r, s) of the tile is row offset vrow[r] (or out of range) + s pixels; only
@@ -96,26 +108,6 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     const int tt = tid >> 3, q = tid & 7;
     const int cs = p.c0;                       // pixel stride (== c1 when c1 != 0)
     const int shift = p.Wi + 1;                // window corner (2ty-1, 2tx-1) >= (-1, -1)
-    unsigned vrow[4];
-    bool col0_ok = false, col3_ok = false;
-    {
-        const int m = m_blk + tt;
-        int ty = 0, tx = 0, b = 0;
-        const bool mv = m < w.tiles;
-        if (mv) {
-            const int t2 = fdiv(m, w.dTw);
-            tx = m - t2 * (p.Wo >> 1);
-            b = fdiv(t2, w.dTh);
-            ty = t2 - b * (p.Ho >> 1);
-        }
-        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
-        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + q * 8);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
-        col0_ok = x0 >= 0;
-        col3_ok = x0 + 3 < p.Wi;
-    }
     const unsigned pixb = (unsigned)cs * 4u;
     const float* a0 = p.src0 - (long long)shift * cs;
     const float* a1 = (p.c1 ? p.src1 : p.src0) - (long long)shift * cs;
@@ -132,19 +124,45 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     const int u_rd = (32 * wn + (lane & 31)) * 32 + rd_sw + 2 * wx * 3 * 2048;
     const int v_rd = (32 * wm + (lane & 31)) * 32 + rd_sw + 2 * wx * 3 * 2048;
 
+    // current item
+    int kz = 0, m_blk = 0, n_blk = 0, kc0 = 0, kc1 = 0;
+    unsigned vrow[4];
+    bool col0_ok = false, col3_ok = false;
+    auto decode = [&](int item) {
+        kz = item / per_split;
+        const int rest = item - kz * per_split;
+        const int mb = rest / p.gn;
+        m_blk = mb * WG_BM;
+        n_blk = (rest - mb * p.gn) * WG_BN;
+        kc0 = kz * w.kc_per;
+        kc1 = min(p.C / 16, kc0 + w.kc_per);
+        const int m = m_blk + tt;
+        int ty = 0, tx = 0, b = 0;
+        const bool mv = m < w.tiles;
+        if (mv) {
+            const int t2 = fdiv(m, w.dTw);
+            tx = m - t2 * (p.Wo >> 1);
+            b = fdiv(t2, w.dTh);
+            ty = t2 - b * (p.Ho >> 1);
+        }
+        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + q * 8);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
+        col0_ok = x0 >= 0;
+        col3_ok = x0 + 3 < p.Wi;
+    };
+
     typedef float f32x2v __attribute__((ext_vector_type(2)));
     f32x2v d[16];
     f32x16 acc[8];                            // [i][jj]
-#pragma unroll
-    for (int x = 0; x < 8; ++x)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
 
-    // the 4x4 window of chunk kc (a chunk past the split's end reads zeros: empty buffer range)
+    // the 4x4 window of chunk kc of the current item
     auto load_d = [&](int kc) {
         const int c = kc * 16;
         const bool second = c >= p.c0;
-        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, kc < kc1 ? w.a_bytes : 0u);
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, w.a_bytes);
         const unsigned cb = (unsigned)((second ? c - p.c0 : c) * 4);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -156,16 +174,15 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
             d[e] = __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0));
         }
     };
-    // U pieces of sub-stage (chunk kc, row i) into slot base sb
+    // U pieces of sub-stage (chunk kc, row i) of the current item into U array base
     auto load_u = [&](int kc, int i, unsigned char* base) {
-        const unsigned bytes = kc < kc1 ? w.u_bytes : 0u;
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
             const int P = wave * 3 + e;
             const int jp = P >> 1, half = P & 1;
             const int j = jp / 3, pl = jp - 3 * (jp / 3);
             const unsigned soff = (unsigned)(((kc * 16 + 4 * i + j) * 3 + pl)) * u_row + (unsigned)(n_blk * 32 + half * 1024);
-            lean_load(w.U, bytes, base + P * 1024, u_lane, soff);
+            lean_load(w.U, w.u_bytes, base + P * 1024, u_lane, soff);
         }
     };
     // V = row i of B^T d B for this thread's 2 channels -> hi/mid/lo planes in V array sb
@@ -211,18 +228,12 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     };
     using I0 = std::integral_constant<int, 0>;
 
-    // prologue: chunk kc0's window, sub-stage (kc0, 0) in slot 0
-    load_d(kc0);
-    load_u(kc0, 0, ldu0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    make_v(I0{}, ldv0);
-
     // one sub-stage (kc, i) in slot i & 1: wait for its U pieces and every wave's V stores;
     // issue the next sub-stage's U; form the next sub-stage's V (into the other slot - a
     // separate LDS array, so the compiler sees it independent of the operand reads) between
     // this sub-stage's two MFMA groups.  The window of chunk kc+1 is loaded into the same
     // registers once row 3 of chunk kc is formed (sub-stage 2) and waited for in sub-stage 3
-    // behind the first MFMA group.
+    // behind the first MFMA group.  Nothing is loaded past the item's last chunk.
     auto sub = [&](int kc, auto i_c) {
         constexpr int i = decltype(i_c)::value;
         unsigned char* cv = (i & 1) ? ldv1 : ldv0;
@@ -233,93 +244,121 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        const bool more = kc + 1 < kc1;
         if constexpr (i < 3) {
             load_u(kc, i + 1, nu);
             mma(std::integral_constant<int, 2 * i>{}, cv, cu, 0);
             make_v(std::integral_constant<int, i + 1>{}, nv);
-            if constexpr (i == 2) load_d(kc + 1);
+            if constexpr (i == 2)
+                if (more) load_d(kc + 1);
             mma(std::integral_constant<int, 2 * i + 1>{}, cv, cu, 1);
         } else {
-            load_u(kc + 1, 0, nu);
+            if (more) load_u(kc + 1, 0, nu);
             mma(std::integral_constant<int, 6>{}, cv, cu, 0);
-            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            make_v(I0{}, nv);
+            if (more) {
+                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                make_v(I0{}, nv);
+            }
             mma(std::integral_constant<int, 7>{}, cv, cu, 1);
         }
     };
 
-    for (int kc = kc0; kc < kc1; ++kc) {
-        sub(kc, std::integral_constant<int, 0>{});
-        sub(kc, std::integral_constant<int, 1>{});
-        sub(kc, std::integral_constant<int, 2>{});
-        sub(kc, std::integral_constant<int, 3>{});
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    if (it >= end) return;
+    decode(it);
+    load_d(kc0);
+    load_u(kc0, 0, ldu0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    make_v(I0{}, ldv0);
 
-    // ---- output transform Y = A^T M A.  Wave wx holds positions j = 2wx, 2wx+1 of every row i
-    // for its (32 tiles x 32 channels); per element s_py[j] = sum_i A^T[py][i] M[i][j].  Wave wx
-    // finishes output row py = wx of the tile: Y[py][0] = (s[0] + s[1]) + s[2],
-    // Y[py][1] = s[1] - (s[2] + s[3]); the partner wave (same wm, wn) supplies the other half.
-    // exchange buffers: wx = 0 writes V slot 0 + U slot 0, wx = 1 the slot-1 pair; per (wm, wn)
-    // [2][16][64] floats (8 KB): two of them per 24 KB array
-    unsigned char* xw = (wm ? (wx ? ldu1 : ldu0) : (wx ? ldv1 : ldv0)) + wn * 8192;
-    const unsigned char* xq = (wm ? (wx ? ldu0 : ldu1) : (wx ? ldv0 : ldv1)) + wn * 8192;
-    float* xs = reinterpret_cast<float*>(xw);
-    const float* xr = reinterpret_cast<const float*>(xq);
-    float own0[16], own1[16];
+    // exchange buffers of the output transform: wx = 0 writes V slot 0 + U slot 0, wx = 1 the
+    // slot-1 pair; per (wm, wn) [2][16][64] floats (8 KB): two of them per 24 KB array
+    float* xs = reinterpret_cast<float*>((wm ? (wx ? ldu1 : ldu0) : (wx ? ldv1 : ldv0)) + wn * 8192);
+    const float* xr = reinterpret_cast<const float*>((wm ? (wx ? ldu0 : ldu1) : (wx ? ldv0 : ldv1)) + wn * 8192);
+
+    while (true) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        float sp[2][2];                                  // [py][jj]
+        for (int x = 0; x < 8; ++x)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            sp[0][jj] = acc[0 * 2 + jj][r] + acc[1 * 2 + jj][r] + acc[2 * 2 + jj][r];
-            sp[1][jj] = acc[1 * 2 + jj][r] - acc[2 * 2 + jj][r] - acc[3 * 2 + jj][r];
+            for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+        for (int kc = kc0; kc < kc1; ++kc) {
+            sub(kc, std::integral_constant<int, 0>{});
+            sub(kc, std::integral_constant<int, 1>{});
+            sub(kc, std::integral_constant<int, 2>{});
+            sub(kc, std::integral_constant<int, 3>{});
         }
-        // wx = 0 (j = 0, 1): keeps row 0, sends row 1 as (s0 + s1, s1);
-        // wx = 1 (j = 2, 3): keeps row 1, sends row 0 as (s2, s2 + s3)
-        const int keep = wx, send = 1 - wx;
-        const float k0 = wx == 0 ? sp[keep][0] + sp[keep][1] : sp[keep][0];
-        const float k1 = wx == 0 ? sp[keep][1] : sp[keep][0] + sp[keep][1];
-        const float s0v = wx == 0 ? sp[send][0] + sp[send][1] : sp[send][0];
-        const float s1v = wx == 0 ? sp[send][1] : sp[send][0] + sp[send][1];
-        xs[(0 * 16 + r) * 64 + lane] = s0v;
-        xs[(1 * 16 + r) * 64 + lane] = s1v;
-        own0[r] = k0;
-        own1[r] = k1;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const int m = m_blk + 32 * wm + (lane & 31);
-    if (m >= w.tiles) return;
-    const int t2 = fdiv(m, w.dTw);
-    const int tx = m - t2 * (p.Wo >> 1);
-    const int b = fdiv(t2, w.dTh);
-    const int ty = t2 - b * (p.Ho >> 1);
-    const long long pix0 = ((long long)b * p.Ho + 2 * ty + wx) * p.Wo + 2 * tx;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+
+        // ---- output transform Y = A^T M A.  Wave wx holds positions j = 2wx, 2wx+1 of every
+        // row i for its (32 tiles x 32 channels); per element s_py[j] = sum_i A^T[py][i] M[i][j].
+        // Wave wx finishes output row py = wx of the tile: Y[py][0] = (s[0] + s[1]) + s[2],
+        // Y[py][1] = s[1] - (s[2] + s[3]); the partner wave (same wm, wn) supplies the other half.
+        float y0v[16], y1v[16];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int n = n_blk + 32 * wn + 8 * g + 4 * (lane >> 5);
-        f32x4 y0, y1;
+        for (int r = 0; r < 16; ++r) {
+            float sp[2][2];                              // [py][jj]
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g + e;
+            for (int jj = 0; jj < 2; ++jj) {
+                sp[0][jj] = acc[0 * 2 + jj][r] + acc[1 * 2 + jj][r] + acc[2 * 2 + jj][r];
+                sp[1][jj] = acc[1 * 2 + jj][r] - acc[2 * 2 + jj][r] - acc[3 * 2 + jj][r];
+            }
+            // wx = 0 (j = 0, 1): keeps row 0, sends row 1 as (s0 + s1, s1);
+            // wx = 1 (j = 2, 3): keeps row 1, sends row 0 as (s2, s2 + s3)
+            const int keep = wx, send = 1 - wx;
+            y0v[r] = wx == 0 ? sp[keep][0] + sp[keep][1] : sp[keep][0];
+            y1v[r] = wx == 0 ? sp[keep][1] : sp[keep][0] + sp[keep][1];
+            xs[(0 * 16 + r) * 64 + lane] = wx == 0 ? sp[send][0] + sp[send][1] : sp[send][0];
+            xs[(1 * 16 + r) * 64 + lane] = wx == 0 ? sp[send][1] : sp[send][0] + sp[send][1];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
             const float o0 = xr[(0 * 16 + r) * 64 + lane];
             const float o1 = xr[(1 * 16 + r) * 64 + lane];
             // wx = 0: own = (s0 + s1, s1), other = (s2, s2 + s3);  wx = 1: own = (s2, s2 + s3)
-            y0[e] = wx == 0 ? own0[r] + o0 : o0 + own0[r];
-            y1[e] = wx == 0 ? own1[r] - o1 : o1 - own1[r];
+            y0v[r] = wx == 0 ? y0v[r] + o0 : o0 + y0v[r];
+            y1v[r] = wx == 0 ? y1v[r] - o1 : o1 - y1v[r];
         }
-        if (p.ksplit == 1) {
-            epi_store4(p, EpiRow{pix0, 0, 0}, n, y0);
-            epi_store4(p, EpiRow{pix0 + 1, 0, 0}, n, y1);
-        } else {
-            float* part = p.part + (long long)kz * p.M * p.N;
-            *reinterpret_cast<f32x4*>(part + pix0 * p.N + n) = y0;
-            *reinterpret_cast<f32x4*>(part + (pix0 + 1) * p.N + n) = y1;
+        const int e_kz = kz, e_m = m_blk + 32 * wm + (lane & 31), e_n = n_blk + 32 * wn + 4 * (lane >> 5);
+        const int next = it + step;
+        const bool has_next = PERSIST && next < end;
+        if (has_next) {
+            // every wave's exchange reads are done before the next item's U lands in slot 0
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            decode(next);
+            load_d(kc0);
+            load_u(kc0, 0, ldu0);
         }
+        if (e_m < w.tiles) {
+            const int t2 = fdiv(e_m, w.dTw);
+            const int tx = e_m - t2 * (p.Wo >> 1);
+            const int b = fdiv(t2, w.dTh);
+            const int ty = t2 - b * (p.Ho >> 1);
+            const long long pix0 = ((long long)b * p.Ho + 2 * ty + wx) * p.Wo + 2 * tx;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = e_n + 8 * g;
+                const f32x4 y0 = {y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]};
+                const f32x4 y1 = {y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]};
+                if (p.ksplit == 1) {
+                    epi_store4(p, EpiRow{pix0, 0, 0}, n, y0);
+                    epi_store4(p, EpiRow{pix0 + 1, 0, 0}, n, y1);
+                } else {
+                    float* part = p.part + (long long)e_kz * p.M * p.N;
+                    *reinterpret_cast<f32x4*>(part + pix0 * p.N + n) = y0;
+                    *reinterpret_cast<f32x4*>(part + (pix0 + 1) * p.N + n) = y1;
+                }
+            }
+        }
+        if (!has_next) break;
+        it = next;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        make_v(I0{}, ldv0);
     }
 }
 
@@ -427,6 +466,15 @@ void wino_plan(const pu_conv_args* a, int* ksplit, int* kc_per) {
     *ksplit = ceil_div(chunks, per);
 }
 
+// persistent blocks (default) or one block per item: PU_WINO_PERSIST=0 (A/B runs)
+static bool wino_persist() {
+    static const bool on = [] {
+        const char* e = getenv("PU_WINO_PERSIST");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     WinoParams w;
     w.p = p;
@@ -447,7 +495,11 @@ int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     w.p.ksplit = ks;
     w.p.part = (float*)a->workspace;
     w.kc_per = per;
-    hipLaunchKernelGGL(wino_x6_kernel, dim3((unsigned)(w.gm * w.p.gn * ks)), dim3(512), 0, s, w);
+    const int items = w.gm * w.p.gn * ks;
+    if (wino_persist() && items > 256)
+        hipLaunchKernelGGL(wino_x6_kernel<true>, dim3(256), dim3(512), 0, s, w);
+    else
+        hipLaunchKernelGGL(wino_x6_kernel<false>, dim3((unsigned)items), dim3(512), 0, s, w);
     return ks;
 }
 

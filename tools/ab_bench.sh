@@ -1,0 +1,13 @@
+#!/bin/bash
+# End-to-end A/B of one environment switch on bench.py (C2 unless more args): alternating runs.
+#   bash tools/ab_bench.sh VAR "v1 v2" [bench args...]
+set -u
+VAR=$1; VALS=$2; shift 2
+for rep in 1 2; do
+  for v in $VALS; do
+    out=$(env $VAR=$v timeout -k 10 240 python bench.py --no-cpu-baseline --no-oja "$@" 2>/dev/null | tail -1) || { echo "bench failed ($VAR=$v)"; exit 1; }
+    python -c "
+import json,sys; d=json.loads(sys.argv[1]); r=d['roofline']
+print('$VAR=$v', d['value'], 'img/s', d['ms_per_step'], 'ms', r['kernel'], r['frac'], r.get('direct_equivalent_frac'))" "$out"
+  done
+done
