@@ -326,7 +326,7 @@ def main():
         mfma = {t: d for t, d in summ.items() if d["flops"] and (t.startswith("igemm") or t.startswith("wgrad"))}
         dom = max(mfma.items(), key=lambda kv: kv[1]["ms"])
         dtag, dd = dom
-        hbm_bound = "direct" in dtag and dd["bytes"] > 0   # small-channel direct convs (C4/C5 levels)
+        hbm_bound = ("direct" in dtag or "x6s" in dtag) and dd["bytes"] > 0   # small-channel convs (C4/C5 levels)
         if args.config == "c3":     # v_mfma_f32_32x32x16_bf16: 4096 FLOP/clk/CU dense
             peak = f32peak * 16.0
             basis = "bf16 MFMA 4096 FLOP/clk/CU x %d CU x %.2f GHz (dense)" % (cu, clk)

@@ -97,8 +97,10 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
  * test: both compute the same sums in the same order when the per-tap launch is not split) */
 /* PU_CONV_HALO_V1: a dispatch hint - take the register-staged 256-pixel halo kernel instead of the
  * DMA-ring 512-pixel one (A/B runs; the per-tap bit-identity test) */
+/* PU_CONV_NO_SMALLX6: a dispatch hint - keep an 8/16-channel 3x3 layer on the VALU direct kernel
+ * instead of the 16x16x32 MFMA one (A/B runs) */
 enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8, PU_CONV_NO_HALO = 16,
-       PU_CONV_HALO_V1 = 32 };
+       PU_CONV_HALO_V1 = 32, PU_CONV_NO_SMALLX6 = 64 };
 
 typedef struct {
     int batch;

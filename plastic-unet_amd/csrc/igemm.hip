@@ -1361,6 +1361,10 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         else hipLaunchKernelGGL((conv1x1_small_kernel<8, 16>), g1, dim3(256), 0, s, p);
         return check_launch("pu_conv_igemm (1x1 small-channel)");
     }
+    if (smallx6_ok(a, p.vec_epi)) {
+        p.ksplit = 1;
+        return smallx6_launch(a, p, s);
+    }
     if (small_conv_ok(a)) {
         p.ksplit = 1;
         const dim3 sgrid((unsigned)(((a->out_w + SC_TW - 1) / SC_TW) * ((a->out_h + SC_TH - 1) / SC_TH) * a->batch));
@@ -1479,6 +1483,13 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         *bm = 256;
         *bn = a->n;
         *mode = 3;
+        if (ksplit) *ksplit = 1;
+        return PU_OK;
+    }
+    if (smallx6_ok(a, vec_epilogue(a))) {   // reported as mode 7 ("x6s"), 16 x 32 pixels x n
+        *bm = 512;
+        *bn = a->n;
+        *mode = 7;
         if (ksplit) *ksplit = 1;
         return PU_OK;
     }

@@ -1,0 +1,174 @@
+// 3x3/s1/p1 convolutions with 8 or 16 input and output channels (the 8/16-channel levels of
+// configs C4 / C5: coord_conv_script.py:155-192, unet_p_res.py:142-189), forward and data
+// gradient, on the exact 6-product bf16 MFMA scheme of the other fp32 convolutions
+// (v_mfma_f32_16x16x32_bf16: each fp32 product as hi/mid/lo bf16 terms, fp32 accumulation).
+//
+// The VALU direct kernel (igemm.hip smallconv_kernel) issued ~38 TFLOP/s on these layers - far
+// from the HBM bound they have (18-36 FLOP/B).  Here a block stages the (16+2) x (32+2) input halo
+// of a 16 x 32 output tile ONCE, split into bf16 planes in LDS (both concat sources, zero
+// padding), and every tap reads its shifted 16-pixel windows from that image:
+//   GEMM  D[n][pixel] = sum_k W[n][k] X[k][pixel],  k = tap * C + c (the packed weight's order)
+//   A = the weights (16 rows n; rows >= N are zero), held in registers as split planes for the
+//       whole block (K padded to 32: 3 k-steps for C = 8, 5 for C = 16; padded k are zero);
+//   B = 16 consecutive output pixels of one row x 32 k: lane (pixel j, k-group g) reads 8 channels
+//       of one tap at halo pixel (row + r, col + j + s) - one conflict-free ds_read_b128 per plane
+//       (channel halves of C = 16 are separate LDS images so 16 lanes read 256 contiguous bytes);
+//   D (16 x 16, 4 registers): lane holds 4 consecutive channels of one pixel -> igemm's float4
+//       epilogue (bias, residual, ReLU, masks, concat split, accumulate).
+// Each wave owns 4 output rows x 32 pixels = 8 groups of 16 pixels: 8 accumulators of 4 registers.
+#include "conv_common.h"
+
+namespace pu {
+
+constexpr int SX_TH = 16, SX_TW = 32;                 // output tile
+constexpr int SX_HH = SX_TH + 2, SX_HW = SX_TW + 2;   // halo
+constexpr int SX_HP = SX_HH * SX_HW;                  // halo pixels (612)
+
+typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
+typedef float f32x4s __attribute__((ext_vector_type(4)));
+
+template <int C, int N>
+__global__ __launch_bounds__(256) void smallconv_x6_kernel(const IgemmParams p) {
+#pragma clang fp contract(off)
+    constexpr int HALVES = C / 8;                   // 8-channel LDS images per plane
+    constexpr int KS = (9 * C + 31) / 32;           // 32-wide k steps
+    // [plane][half][pixel][8 channels] bf16
+    __shared__ __attribute__((aligned(16))) __bf16 img[3 * HALVES * SX_HP * 8];
+
+    const int tiles_w = (p.Wo + SX_TW - 1) / SX_TW;
+    const int tiles_h = (p.Ho + SX_TH - 1) / SX_TH;
+    int blk = blockIdx.x;
+    const int txi = blk % tiles_w;
+    blk /= tiles_w;
+    const int tyi = blk % tiles_h;
+    const int b = blk / tiles_h;
+    const int y0 = tyi * SX_TH - 1, x0 = txi * SX_TW - 1;   // halo origin (pad 1)
+    const long long imgpix = (long long)b * p.Hi * p.Wi;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+
+    // ---- weights: lane (row n = lane & 15, k-group g = lane >> 4) holds k = 32s + 8g .. +7 of
+    // every step s as hi/mid/lo planes (rows >= N and k >= 9C are zero)
+    bf16x8s wa[KS][3];
+    {
+        const int n = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            f32x4s lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
+            const int k = 32 * s + 8 * g;
+            if (n < N && k < 9 * C) {      // 9C is a multiple of 8: the 8 k are all real or all padding
+                lo = *reinterpret_cast<const f32x4s*>(p.wt + n * p.k_pad + k);
+                hi = *reinterpret_cast<const f32x4s*>(p.wt + n * p.k_pad + k + 4);
+            }
+            split3_pairs(lo, hi, wa[s][0], wa[s][1], wa[s][2]);
+        }
+    }
+
+    // ---- stage the halo, split once: float4 e = (pixel, channel quad) of one of the sources
+    {
+        constexpr int Q = C / 4;
+        constexpr int NE = SX_HP * Q;
+        constexpr int PT = (NE + 511) / 512;        // pairs of float4 per thread
+        f32x4s v[PT][2];
+#pragma unroll
+        for (int it = 0; it < PT; ++it)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = (it * 2 + u) * 256 + tid;
+                const int q = e % Q, pix = e / Q;
+                const int hx = pix % SX_HW, hy = pix / SX_HW;
+                const int gy = y0 + hy, gx = x0 + hx;
+                v[it][u] = f32x4s{0.f, 0.f, 0.f, 0.f};
+                if (e < NE && (unsigned)gy < (unsigned)p.Hi && (unsigned)gx < (unsigned)p.Wi) {
+                    const long long px = imgpix + (long long)gy * p.Wi + gx;
+                    const int c = 4 * q;
+                    v[it][u] = c < p.c0 ? *reinterpret_cast<const f32x4s*>(p.src0 + px * p.c0 + c)
+                                        : *reinterpret_cast<const f32x4s*>(p.src1 + px * p.c1 + (c - p.c0));
+                }
+            }
+#pragma unroll
+        for (int it = 0; it < PT; ++it) {
+            bf16x8_t h, m, l;
+            split3_pairs(v[it][0], v[it][1], h, m, l);
+            typedef unsigned u32x4s __attribute__((ext_vector_type(4)));
+            typedef unsigned u32x2s __attribute__((ext_vector_type(2)));
+            const u32x4s pv[3] = {__builtin_bit_cast(u32x4s, h), __builtin_bit_cast(u32x4s, m), __builtin_bit_cast(u32x4s, l)};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = (it * 2 + u) * 256 + tid;
+                if (e >= NE) continue;
+                const int q = e % Q, pix = e / Q;
+                const int half = q >> 1, sub = q & 1;
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    *reinterpret_cast<u32x2s*>(img + ((pl * HALVES + half) * SX_HP + pix) * 8 + sub * 4) =
+                        u32x2s{pv[pl][2 * u], pv[pl][2 * u + 1]};
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- MFMAs: wave w owns output rows 4w .. 4w+3, each 2 groups of 16 pixels (8 groups)
+    const int j = lane & 15, g = lane >> 4;
+    f32x4s acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = f32x4s{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+        const int k = 32 * s + 8 * g;               // this lane's 8 k: one tap, 8 channels
+        const int tap = k / C, c8 = (k % C) / 8;
+        const bool live = tap < 9;
+        const int r = live ? tap / 3 : 0, sx = live ? tap % 3 : 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int row = 4 * wave + (t >> 1), col = (t & 1) * 16 + j;
+            const int hp = (row + r) * SX_HW + col + sx;
+            bf16x8s xb[3];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                xb[pl] = *reinterpret_cast<const bf16x8s*>(img + ((pl * HALVES + c8) * SX_HP + hp) * 8);
+                if (!live) xb[pl] = bf16x8s{};
+            }
+            f32x4s c = acc[t];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][1], xb[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][2], xb[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][0], xb[2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][1], xb[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][0], xb[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][0], xb[0], c, 0, 0, 0);
+            acc[t] = c;
+        }
+    }
+
+    // ---- epilogue: lane holds channels 4g .. 4g+3 of pixel (row, col)
+    if (4 * g >= N) return;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const int oy = tyi * SX_TH + 4 * wave + (t >> 1), ox = txi * SX_TW + (t & 1) * 16 + j;
+        if (oy >= p.Ho || ox >= p.Wo) continue;
+        const int m = (b * p.Ho + oy) * p.Wo + ox;
+        epi_store4(p, epi_row(p, m), 4 * g, acc[t]);
+    }
+}
+
+// C in {8, 16} from one source or two 8-channel-aligned ones, N in {8, 16}, 3x3 / s1 / p1 same
+// size, tap-major fp32 weight rows (k_pad = 9C rounded to 16), float4 epilogue, no ConvT shuffle
+bool smallx6_ok(const pu_conv_args* a, bool vec_epi) {
+    const int C = a->c0 + a->c1;
+    return !(a->flags & PU_CONV_NO_SMALLX6) && a->weight6 && (C == 8 || C == 16) && (a->n == 8 || a->n == 16) && a->c0 % 8 == 0 &&
+           a->c1 % 8 == 0 && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
+           a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) && vec_epi &&
+           (a->cgroup == 0 || a->cgroup >= C) && a->k_pad == (9 * C + 15) / 16 * 16;
+}
+
+int smallx6_launch(const pu_conv_args* a, const IgemmParams& p, hipStream_t s) {
+    const int C = a->c0 + a->c1;
+    const dim3 grid((unsigned)(((a->out_w + SX_TW - 1) / SX_TW) * ((a->out_h + SX_TH - 1) / SX_TH) * a->batch));
+    if (C == 8 && a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 8>), grid, dim3(256), 0, s, p);
+    else if (C == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 16>), grid, dim3(256), 0, s, p);
+    else if (a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<16, 8>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((smallconv_x6_kernel<16, 16>), grid, dim3(256), 0, s, p);
+    return check_launch("pu_conv_igemm (small-channel x6)");
+}
+
+}  // namespace pu

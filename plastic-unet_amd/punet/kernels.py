@@ -10,7 +10,8 @@ import torch
 
 from . import _lib
 from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, WinoJob, check,
-                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1)
+                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1,
+                   PU_CONV_NO_SMALLX6)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
@@ -23,7 +24,7 @@ def lib():
 
 # ------------------------------------------------------------------------------ launch profiler
 _PROF = None
-_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem", 6: "wino"}
+_MODES = {0: "chunk16", 1: "vec4", 2: "scalar", 3: "direct", 4: "x6", 5: "stem", 6: "wino", 7: "x6s"}
 
 # fp32 GEMM arithmetic of the MFMA convolutions: "split6" (default) = each fp32 product as 6 exact
 # bf16 products on the bf16 MFMA pipe (pu_split_weight6 / pu_conv_args.weight6, fp32-accurate);
@@ -56,7 +57,19 @@ def fp32_math():
 # fp32 3x3/s1/p1 convolutions (forward and data gradient) on the Winograd F(2x2,3x3) kernel where
 # the layer qualifies (PU_WINO=0: the direct 6-product kernels everywhere; A/B runs, tests flip it
 # with set_wino)
-_WINO = os.environ.get("PU_WINO", "1") != "0"
+_WINO = os.environ.get("PU_WINO", "0") != "0"
+
+
+# fp32 8/16-channel 3x3 convolutions on the 16x16x32 MFMA kernel (csrc/smallconv.hip) or the VALU
+# direct kernel (PU_SMALLX6=0; tests flip it with set_smallx6)
+_SMALLX6 = os.environ.get("PU_SMALLX6", "0") != "0"
+
+
+def set_smallx6(on):
+    """Route 8/16-channel fp32 3x3 convolutions to the MFMA kernel (True) or the VALU direct one."""
+    global _SMALLX6
+    prev, _SMALLX6 = _SMALLX6, bool(on)
+    return prev
 
 
 def set_wino(on):
@@ -209,7 +222,7 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
         _req(t, nm, dt)
     _req(bias, "bias")
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
-        | (PU_EPI_RESID if resid is not None else 0) | _halo_flags()
+        | (PU_EPI_RESID if resid is not None else 0) | _halo_flags() | (0 if _SMALLX6 else PU_CONV_NO_SMALLX6)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,
@@ -236,7 +249,7 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
     M = batch * out_hw[0] * out_hw[1]
     tag = "igemm<%dx%d,%s%s>" % (bm.value, bn.value, _MODES[mode.value], ",k%d" % ks.value if ks.value > 1 else "")
     nb = 0.0
-    if mode.value in (3, 5):    # direct small-channel / stem kernels: HBM-bound, report algorithmic bytes
+    if mode.value in (3, 5, 7):    # small-channel / stem kernels: HBM-bound, report algorithmic bytes
         per = (c0 + c1) + n * (1 + int(accum) + int(resid is not None)) + n0_mask(n, n0, mask0, mask1)
         nb = 4.0 * M * per
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1), nbytes=nb):

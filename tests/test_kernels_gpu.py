@@ -68,6 +68,15 @@ CONV_CASES = [
     (32, 64, 64, 32, 0, 32),    # 256 x 32 lean tile (>= 480 tiles), the C4 64^2 level
 ]
 
+# 8/16-channel layers on the 16x16x32 MFMA kernel (csrc/smallconv.hip; K.set_smallx6)
+SMALL_X6_CASES = [
+    (2, 40, 70, 8, 0, 8),       # 8 -> 8: partial 16 x 32 tiles
+    (1, 33, 65, 8, 8, 16),      # two 8-channel sources -> 16 (dgrad: 16 -> 8 + 8 with the split)
+    (2, 64, 64, 16, 0, 8),      # 16 -> 8 (dgrad 8 -> 16)
+    (1, 17, 36, 16, 0, 16),     # 16 -> 16, odd height
+    (2, 37, 45, 16, 0, 16),     # ragged edges on both axes
+]
+
 
 @pytest.mark.parametrize("B,H,W,c0,c1,cout", CONV_CASES)
 def test_conv3x3_fwd_dgrad_wgrad(B, H, W, c0, c1, cout):
@@ -102,6 +111,15 @@ def test_conv3x3_fwd_dgrad_wgrad(B, H, W, c0, c1, cout):
     dw, db = T.conv3x3_wgrad(dzk, dx0, dx1)
     assert_close(dw, wr.grad)
     assert_close(db, br.grad)
+
+
+@pytest.mark.parametrize("B,H,W,c0,c1,cout", SMALL_X6_CASES)
+def test_conv3x3_small_channel_x6(B, H, W, c0, c1, cout):
+    prev = K.set_smallx6(True)
+    try:
+        test_conv3x3_fwd_dgrad_wgrad(B, H, W, c0, c1, cout)
+    finally:
+        K.set_smallx6(prev)
 
 
 # (1, 4, 512, 64): tiny pixel grid, deep K -> split-K igemm for the shuffled forward and the dgrad
