@@ -14,7 +14,7 @@ spec = importlib.util.spec_from_file_location("pu_lib", os.path.join(os.path.dir
 L = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(L)
 lib = L.load()
-assert lib.pu_abi_version() == 1
+assert lib.pu_abi_version() == L.ABI_VERSION
 assert len(lib.pu_build_id()) == 16
 
 A = 0x10000  # 16-byte aligned stand-in device pointers: nothing here dereferences them
