@@ -158,21 +158,24 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     f32x2v d[16];
     f32x16 acc[8];                            // [i][jj]
 
-    // the 4x4 window of chunk kc of the current item
-    auto load_d = [&](int kc) {
+    // window row rr (4 pixels x 2 channels) of chunk kc of the current item
+    auto load_row = [&](int kc, int rr) {
         const int c = kc * 16;
         const bool second = c >= p.c0;
         const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, w.a_bytes);
         const unsigned cb = (unsigned)((second ? c - p.c0 : c) * 4);
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int rr = e >> 2, ss = e & 3;
+        for (int ss = 0; ss < 4; ++ss) {
             unsigned vo = vrow[rr];
             if (ss == 0) vo = col0_ok ? vo : LEAN_OOB;
             if (ss == 3) vo = col3_ok ? vo : LEAN_OOB;
             const unsigned soff = __builtin_amdgcn_readfirstlane(cb + ss * pixb);
-            d[e] = __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0));
+            d[rr * 4 + ss] = __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0));
         }
+    };
+    auto load_d = [&](int kc) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) load_row(kc, rr);
     };
     // U pieces of sub-stage (chunk kc, row i) of the current item into U array base
     auto load_u = [&](int kc, int i, unsigned char* base) {
@@ -231,34 +234,42 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     // one sub-stage (kc, i) in slot i & 1: wait for its U pieces and every wave's V stores;
     // issue the next sub-stage's U; form the next sub-stage's V (into the other slot - a
     // separate LDS array, so the compiler sees it independent of the operand reads) between
-    // this sub-stage's two MFMA groups.  The window of chunk kc+1 is loaded into the same
-    // registers once row 3 of chunk kc is formed (sub-stage 2) and waited for in sub-stage 3
-    // behind the first MFMA group.  Nothing is loaded past the item's last chunk.
+    // this sub-stage's two MFMA groups.  Each window row of chunk kc+1 is reloaded into the same
+    // registers as soon as chunk kc's last transform that reads it is formed (V row i reads
+    // window rows {0,2}, {1,2}, {2,1}, {1,3} for i = 0..3): row 0 in sub-stage 0, row 2 in
+    // sub-stage 1, rows 1 and 3 in sub-stage 2, so every load has two or more sub-stages of
+    // MFMAs to land in.  VN = the loads issued after the U pieces waited for.  Nothing is loaded
+    // past the item's last chunk.
     auto sub = [&](int kc, auto i_c) {
         constexpr int i = decltype(i_c)::value;
         unsigned char* cv = (i & 1) ? ldv1 : ldv0;
         unsigned char* cu = (i & 1) ? ldu1 : ldu0;
         unsigned char* nv = (i & 1) ? ldv0 : ldv1;
         unsigned char* nu = (i & 1) ? ldu0 : ldu1;
-        if constexpr (i == 3) asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if constexpr (i == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else if constexpr (i == 3) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const bool more = kc + 1 < kc1;
         if constexpr (i < 3) {
             load_u(kc, i + 1, nu);
+            if constexpr (i == 0)
+                if (more) load_row(kc + 1, 0);
             mma(std::integral_constant<int, 2 * i>{}, cv, cu, 0);
             make_v(std::integral_constant<int, i + 1>{}, nv);
+            if constexpr (i == 1)
+                if (more) load_row(kc + 1, 2);
             if constexpr (i == 2)
-                if (more) load_d(kc + 1);
+                if (more) {
+                    load_row(kc + 1, 1);
+                    load_row(kc + 1, 3);
+                }
             mma(std::integral_constant<int, 2 * i + 1>{}, cv, cu, 1);
         } else {
             if (more) load_u(kc + 1, 0, nu);
             mma(std::integral_constant<int, 6>{}, cv, cu, 0);
-            if (more) {
-                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-                make_v(I0{}, nv);
-            }
+            if (more) make_v(I0{}, nv);
             mma(std::integral_constant<int, 7>{}, cv, cu, 1);
         }
     };
