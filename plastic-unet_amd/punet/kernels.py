@@ -57,7 +57,7 @@ def fp32_math():
 # fp32 3x3/s1/p1 convolutions (forward and data gradient) on the Winograd F(2x2,3x3) kernel where
 # the layer qualifies (PU_WINO=0: the direct 6-product kernels everywhere; A/B runs, tests flip it
 # with set_wino)
-_WINO = os.environ.get("PU_WINO", "0") != "0"
+_WINO = os.environ.get("PU_WINO", "1") != "0"
 
 
 # fp32 8/16-channel 3x3 convolutions on the 16x16x32 MFMA kernel (csrc/smallconv.hip) or the VALU

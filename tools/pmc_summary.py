@@ -34,7 +34,7 @@ def main():
     out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     res, dur = load(out)
     for name, c in sorted(res.items()):
-        if "igemm" not in name and "wgrad" not in name and "head" not in name and "trace" not in name:
+        if not any(k in name for k in ("igemm", "wgrad", "head", "trace", "wino", "smallconv")):
             continue
         print(name[:150])
         for k, v in sorted(c.items()):
