@@ -62,7 +62,7 @@ _WINO = os.environ.get("PU_WINO", "1") != "0"
 
 # fp32 8/16-channel 3x3 convolutions on the 16x16x32 MFMA kernel (csrc/smallconv.hip) or the VALU
 # direct kernel (PU_SMALLX6=0; tests flip it with set_smallx6)
-_SMALLX6 = os.environ.get("PU_SMALLX6", "0") != "0"
+_SMALLX6 = os.environ.get("PU_SMALLX6", "1") != "0"
 
 
 def set_smallx6(on):
@@ -87,7 +87,7 @@ def wino_wanted(w, mode):
     if mode not in (0, 1) or w.dim() != 4 or w.shape[2:] != (3, 3) or _FP32_MATH != "split6":
         return False
     n, c = (w.shape[0], w.shape[1]) if mode == 0 else (w.shape[1], w.shape[0])
-    return c % 32 == 0 and n % 64 == 0
+    return c % 32 == 0 and n % 64 == 0 and (c >= 128 or n <= 64)   # csrc wino_ok
 
 
 def pack_wino(jobs):

@@ -43,7 +43,7 @@ def check(name, got, cpu32, ref64):
 CASES = [
     # B, H, W, c0, c1, cout
     (2, 16, 16, 64, 0, 64),       # one block of 64 tiles x 2 images
-    (3, 10, 14, 32, 0, 128),      # 105 tiles: a partial second tile block, 2 channel blocks, non-square
+    (3, 10, 14, 128, 0, 128),     # 105 tiles: a partial second tile block, 2 channel blocks, non-square
     (2, 8, 8, 64, 64, 64),        # concat (two sources), every tile on an image edge
     (1, 32, 16, 128, 0, 192),     # 3 channel blocks, 8 chunks
     (4, 8, 8, 512, 0, 512),       # split-K (bottom level shape): 64 tiles, 8 channel blocks
@@ -81,8 +81,8 @@ def test_wino_fwd_dgrad_vs_fp64(B, H, W, c0, c1, cout):
         dzk = nhwc(dz).to(DEV)
         d0, d1 = T.conv3x3_dgrad(dzk, wk, pk, split=c0 if c1 else None, mask0=x0, mask1=x1)
         dx = torch.cat([d0, d1], 3) if c1 else d0
-        if cout % 32 == 0 and C % 64 == 0:
-            assert getattr(pk.get(wk, 1, K.round16(9 * cout), K.cgroup_for(cout)), "_wino", None) is not None
+        assert (getattr(pk.get(wk, 1, K.round16(9 * cout), K.cgroup_for(cout)), "_wino", None) is not None) \
+            == K.wino_wanted(wk, 1)
         check("wino dgrad", nchw(dx), ref[torch.float32][1], ref[torch.float64][1])
     finally:
         K.set_wino(prev)
