@@ -145,9 +145,11 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     auto decode = [&](int item) {
         kz = item / per_split;
         const int rest = item - kz * per_split;
-        const int mb = rest / p.gn;
-        m_blk = mb * WG_BM;
-        n_blk = (rest - mb * p.gn) * WG_BN;
+        // channel block slowest: the items an XCD runs at once share one channel block, so its U
+        // slice (C x 64 x 96 B) stays in that XCD's L2 instead of every block streaming all of U
+        const int nb = rest / w.gm;
+        m_blk = (rest - nb * w.gm) * WG_BM;
+        n_blk = nb * WG_BN;
         kc0 = kz * w.kc_per;
         kc1 = min(p.C / 16, kc0 + w.kc_per);
         const int m = m_blk + tt;
@@ -410,11 +412,14 @@ __global__ __launch_bounds__(256) void wino_pack_kernel(const WinoPackBatch bt) 
     int j = 0, b0 = 0;
     while (j + 1 < bt.count && (int)blockIdx.x >= b0 + bt.job[j].blocks) b0 += bt.job[j++].blocks;
     const WinoPackJob J = bt.job[j];
-    const int idx = ((int)blockIdx.x - b0) * 256 + threadIdx.x;   // (c8 group, n): n fastest
+    // lane = (chunk, n, half): neighbouring lanes write neighbouring 16-byte halves of one
+    // 32-byte U row, so every store instruction covers a contiguous 1 KB
+    const int idx = ((int)blockIdx.x - b0) * 256 + threadIdx.x;
     const int c8s = J.c / 8;
     if (idx >= J.n * c8s) return;
-    const int n = idx % J.n;
-    const int c8 = idx / J.n;
+    const int nh = idx >> 1;
+    const int n = nh % J.n;
+    const int c8 = (nh / J.n) * 2 + (idx & 1);
     typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
     const int chunk = c8 >> 1, half = c8 & 1;
     // one row a of G g G^T at a time (12 output vectors live instead of 48)
