@@ -64,17 +64,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-// PERSIST: one block per CU walks work items (tile block, channel block, K split); each XCD takes a
-// contiguous range of items (neighbouring tiles share input windows in that XCD's L2) and the
-// next item's first window and U pieces are in flight while the current item's epilogue runs.
-// Otherwise one item per block (XCD-aware order).
+// One block walks work items (tile block x channel block x K split): PERSIST - one block per CU,
+// each XCD a contiguous range of items, channel block slowest (the items an XCD runs at once share
+// one U slice in its L2); otherwise one item per block (XCD-aware order).
 //
-// Pipeline per sub-stage s (chunk kc, row i): V of s was formed during s-1 (two V slots), U of s
-// was issued two sub-stages earlier (three U slots: the LDS-DMA has two sub-stages of MFMAs to
-// land in).  Every load is issued unconditionally (past the item's last chunk the buffer range is
-// empty and zeros land), so the wait counts are compile-time exact:
-//   issued after U(s): the window rows of sub-stage s-2, U(s+1), the window rows of s-1, with
-//   4 / 4 / 8 / 0 row loads in sub-stages i = 0 / 1 / 2 / 3.
+// The chunks of consecutive items form one stream: the loads a chunk issues for "the next chunk"
+// (its window rows, the first U pieces) target the next item's first chunk at an item's end, so
+// the next item's first sub-stages are in flight during this item's last chunk and epilogue
+// instead of waiting out a cold HBM round trip per item.
+//
+// Sub-stage s (chunk kc, row i): V of s was formed during s-1 (V slots i & 1), U of s was issued
+// three sub-stages earlier (U slots i: a 4-slot ring).  Every load is issued unconditionally
+// (past the last item the buffer range is empty and zeros land), so the wait counts are
+// compile-time exact: issued after U(s) are the window rows of s-3, s-2, s-1 (4 / 4 / 8 / 0 row
+// loads in sub-stages i = 0 / 1 / 2 / 3) and U(s+1), U(s+2) (3 pieces each).
 template <bool PERSIST>
 __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 #pragma clang fp contract(off)
@@ -86,6 +89,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     __shared__ __attribute__((aligned(16))) unsigned char ldu0[WG_HALF];
     __shared__ __attribute__((aligned(16))) unsigned char ldu1[WG_HALF];
     __shared__ __attribute__((aligned(16))) unsigned char ldu2[WG_HALF];
+    __shared__ __attribute__((aligned(16))) unsigned char ldu3[WG_HALF];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -108,10 +112,9 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         end = it + 1;
         step = 1;
     }
+    if (it >= end) return;
 
     // ---- producer role: tile tt of the block, channels 2q, 2q+1 of each 16-channel chunk.
-    // Window pixel (r, s) of the tile is row offset vrow[r] (or out of range) + s pixels; only
-    // rows 0 / 3 and columns 0 / 3 can leave the image.
     const int tt = tid >> 3, q = tid & 7;
     const int cs = p.c0;                       // pixel stride (== c1 when c1 != 0)
     const int shift = p.Wi + 1;                // window corner (2ty-1, 2tx-1) >= (-1, -1)
@@ -121,8 +124,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     // V store address of this thread inside a slot (row tt, its 4-byte pair, swizzled half)
     const int v_st = tt * 32 + (((q >> 2) ^ ((tt >> 3) & 1)) * 16) + (q & 3) * 4;
 
-    // ---- U loader: wave w fills pieces 3w .. 3w+2 (piece P = (j*3 + plane)*2 + row half); the
-    // piece's offset inside a sub-stage's U block is fixed per wave
+    // ---- U loader: wave w fills pieces 3w .. 3w+2 (piece P = (j*3 + plane)*2 + row half)
     const unsigned u_lane = (unsigned)((lane >> 1) * 32 + (((lane & 1) ^ ((lane >> 4) & 1)) * 16));
     const unsigned u_row = (unsigned)p.N * 32u;                  // bytes per (xi, plane) block
     unsigned poff[3];
@@ -138,23 +140,24 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     const int u_rd = (32 * wn + (lane & 31)) * 32 + rd_sw + 2 * wx * 3 * 2048;
     const int v_rd = (32 * wm + (lane & 31)) * 32 + rd_sw + 2 * wx * 3 * 2048;
 
-    // current item
-    int kz = 0, m_blk = 0, n_blk = 0, kc0 = 0, kc1 = 0;
-    unsigned vrow[4];
-    bool col0_ok = false, col3_ok = false;
-    auto decode = [&](int item) {
-        kz = item / per_split;
-        const int rest = item - kz * per_split;
-        // channel block slowest: the items an XCD runs at once share one channel block, so its U
-        // slice (C x 64 x 96 B) stays in that XCD's L2 instead of every block streaming all of U
-        const int nb = rest / w.gm;
-        m_blk = (rest - nb * w.gm) * WG_BM;
-        n_blk = nb * WG_BN;
-        kc0 = kz * w.kc_per;
-        kc1 = min(p.C / 16, kc0 + w.kc_per);
-        const int m = m_blk + tt;
+    // an item as the loaders see it: its chunk range, channel block and this thread's window rows
+    struct Item {
+        int kz, m_blk, n_blk, kc0, kc1;
+        unsigned vrow[4];
+        bool c0ok, c3ok, live;
+    };
+    auto decode = [&](int item, Item& I) {
+        I.live = item < end;
+        I.kz = item / per_split;
+        const int rest = item - I.kz * per_split;
+        const int nb = rest / w.gm;          // channel block slowest (U slice shared in L2)
+        I.m_blk = (rest - nb * w.gm) * WG_BM;
+        I.n_blk = nb * WG_BN;
+        I.kc0 = I.kz * w.kc_per;
+        I.kc1 = min(p.C / 16, I.kc0 + w.kc_per);
+        const int m = I.m_blk + tt;
         int ty = 0, tx = 0, b = 0;
-        const bool mv = m < w.tiles;
+        const bool mv = I.live && m < w.tiles;
         if (mv) {
             const int t2 = fdiv(m, w.dTw);
             tx = m - t2 * (p.Wo >> 1);
@@ -165,34 +168,38 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + q * 8);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
-        col0_ok = x0 >= 0;
-        col3_ok = x0 + 3 < p.Wi;
+            I.vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
+        I.c0ok = x0 >= 0;
+        I.c3ok = x0 + 3 < p.Wi;
     };
+    Item cur, nxt;
+    decode(it, cur);
+    decode(it + step, nxt);
 
     typedef float f32x2v __attribute__((ext_vector_type(2)));
     f32x2v d[16];
     f32x16 acc[8];                            // [i][jj]
 
-    // window row rr (4 pixels x 2 channels) of chunk kc of the current item (zeros past kc1)
-    auto load_row = [&](int kc, int rr) {
+    // window row rr (4 pixels x 2 channels) of chunk kc of item I (zeros past its chunks)
+    auto load_row = [&](const Item& I, int kc, int rr) {
         const int c = kc * 16;
         const bool second = c >= p.c0;
-        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, kc < kc1 ? w.a_bytes : 0u);
+        const bool ok = I.live && kc < I.kc1;
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, ok ? w.a_bytes : 0u);
         const unsigned cb = (unsigned)((second ? c - p.c0 : c) * 4);
 #pragma unroll
         for (int ss = 0; ss < 4; ++ss) {
-            unsigned vo = vrow[rr];
-            if (ss == 0) vo = col0_ok ? vo : LEAN_OOB;
-            if (ss == 3) vo = col3_ok ? vo : LEAN_OOB;
+            unsigned vo = I.vrow[rr];
+            if (ss == 0) vo = I.c0ok ? vo : LEAN_OOB;
+            if (ss == 3) vo = I.c3ok ? vo : LEAN_OOB;
             const unsigned soff = __builtin_amdgcn_readfirstlane(cb + ss * pixb);
             d[rr * 4 + ss] = __builtin_bit_cast(f32x2v, __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0));
         }
     };
-    // U pieces of sub-stage (chunk kc, row i) of the current item into U slot base (zeros past kc1)
-    auto load_u = [&](int kc, int i, unsigned char* base) {
-        const unsigned bytes = kc < kc1 ? w.u_bytes : 0u;
-        const unsigned sb = (unsigned)((kc * 16 + 4 * i) * 3) * u_row + (unsigned)(n_blk * 32);
+    // U pieces of sub-stage (chunk kc, row i) of item I into U slot base (zeros past its chunks)
+    auto load_u = [&](const Item& I, int kc, int i, unsigned char* base) {
+        const unsigned bytes = I.live && kc < I.kc1 ? w.u_bytes : 0u;
+        const unsigned sb = (unsigned)((kc * 16 + 4 * i) * 3) * u_row + (unsigned)(I.n_blk * 32);
 #pragma unroll
         for (int e = 0; e < 3; ++e) lean_load(w.U, bytes, base + (wave * 3 + e) * 1024, u_lane, sb + poff[e]);
     };
@@ -238,77 +245,72 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         acc[x] = c;
     };
     using I0 = std::integral_constant<int, 0>;
+    auto uslot = [&](int k) -> unsigned char* { return k == 0 ? ldu0 : k == 1 ? ldu1 : k == 2 ? ldu2 : ldu3; };
 
-    // sub-stage (kc, i) at position S = 4 * cc + i of a 3-chunk loop trip: V slot i & 1, U slot
-    // S % 3; issues U(S + 2) into slot (S + 2) % 3 and the window rows of chunk kc+1 that chunk
-    // kc no longer reads (row 0 in i = 0, row 2 in i = 1, rows 1 and 3 in i = 2)
-    auto sub = [&](int kc, auto i_c, auto s_c) {
+    // sub-stage (kc, i) of the current item; T / tkc = the stream's next chunk (this item's kc+1,
+    // or the next item's first chunk).  Issues U(s+3) into slot (i+3) & 3 (the slot sub-stage
+    // s-1 read) and the window rows of the next chunk that chunk kc no longer reads (row 0 in
+    // i = 0, row 2 in i = 1, rows 1 and 3 in i = 2).
+    auto sub = [&](int kc, const Item& T, int tkc, auto i_c) {
         constexpr int i = decltype(i_c)::value;
-        constexpr int S = decltype(s_c)::value;
         unsigned char* cv = (i & 1) ? ldv1 : ldv0;
         unsigned char* nv = (i & 1) ? ldv0 : ldv1;
-        unsigned char* cu = S % 3 == 0 ? ldu0 : S % 3 == 1 ? ldu1 : ldu2;
-        unsigned char* fu = (S + 2) % 3 == 0 ? ldu0 : (S + 2) % 3 == 1 ? ldu1 : ldu2;
-        if constexpr (i == 0) asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory");
-        else if constexpr (i == 1) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
-        else if constexpr (i == 2) asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory");
+        unsigned char* cu = uslot(i);
+        unsigned char* fu = uslot((i + 3) & 3);
+        if constexpr (i == 0) asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
+        else if constexpr (i == 1) asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
+        else if constexpr (i == 2) asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(22) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        load_u(i < 2 ? kc : kc + 1, (i + 2) & 3, fu);
+        if constexpr (i == 0) load_u(cur, kc, 3, fu);
+        else load_u(T, tkc, i - 1, fu);
         asm volatile("" ::: "memory");                  // the wait counts assume U is issued first
-        if constexpr (i == 0) load_row(kc + 1, 0);
+        if constexpr (i == 0) load_row(T, tkc, 0);
         mma(std::integral_constant<int, 2 * i>{}, cv, cu, 0);
         if constexpr (i < 3) make_v(std::integral_constant<int, i + 1>{}, nv);
         else make_v(I0{}, nv);
-        if constexpr (i == 1) load_row(kc + 1, 2);
+        if constexpr (i == 1) load_row(T, tkc, 2);
         if constexpr (i == 2) {
-            load_row(kc + 1, 1);
-            load_row(kc + 1, 3);
+            load_row(T, tkc, 1);
+            load_row(T, tkc, 3);
         }
         mma(std::integral_constant<int, 2 * i + 1>{}, cv, cu, 1);
     };
-    auto chunk = [&](int kc, auto cc_c) {
-        constexpr int cc = decltype(cc_c)::value;
-        sub(kc, std::integral_constant<int, 0>{}, std::integral_constant<int, 4 * cc + 0>{});
-        sub(kc, std::integral_constant<int, 1>{}, std::integral_constant<int, 4 * cc + 1>{});
-        sub(kc, std::integral_constant<int, 2>{}, std::integral_constant<int, 4 * cc + 2>{});
-        sub(kc, std::integral_constant<int, 3>{}, std::integral_constant<int, 4 * cc + 3>{});
-    };
-    // item prologue: the whole window of kc0, U of sub-stages 0 and 1, V of sub-stage 0
-    auto prologue = [&]() {
-        load_row(kc0, 0);
-        load_row(kc0, 1);
-        load_row(kc0, 2);
-        load_row(kc0, 3);
-        load_u(kc0, 0, ldu0);
-        load_u(kc0, 1, ldu1);
-    };
 
-    if (it >= end) return;
-    decode(it);
-    prologue();
+    // stream prologue: the first item's whole first window, U of sub-stages 0..2, V of 0
+    load_row(cur, cur.kc0, 0);
+    load_row(cur, cur.kc0, 1);
+    load_row(cur, cur.kc0, 2);
+    load_row(cur, cur.kc0, 3);
+    load_u(cur, cur.kc0, 0, ldu0);
+    load_u(cur, cur.kc0, 1, ldu1);
+    load_u(cur, cur.kc0, 2, ldu2);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     make_v(I0{}, ldv0);
 
-    // exchange buffers of the output transform: per (wm, wn, wx) [2][16][64] floats (8 KB), the
-    // two waves of one (wm, wn) in one V or U slot
-    const int xq = wm * 2 + wn;
-    unsigned char* xb = xq == 0 ? ldv0 : xq == 1 ? ldv1 : xq == 2 ? ldu0 : ldu1;
-    float* xs = reinterpret_cast<float*>(xb + wx * 8192);
-    const float* xr = reinterpret_cast<const float*>(xb + (1 - wx) * 8192);
+    // output-transform exchange through V slot 1 (free at an item boundary: the last sub-stage
+    // read it, the next item's first V is in slot 0), 4 registers per round:
+    // [wm][wn][wx][2][4][64] floats = 16 KB
+    float* xs = reinterpret_cast<float*>(ldv1) + ((wm * 2 + wn) * 2 + wx) * 512;
+    const float* xr = reinterpret_cast<const float*>(ldv1) + ((wm * 2 + wn) * 2 + (1 - wx)) * 512;
 
     while (true) {
 #pragma unroll
         for (int x = 0; x < 8; ++x)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
-        for (int kc = kc0; kc < kc1; kc += 3) {
-            chunk(kc, std::integral_constant<int, 0>{});
-            if (kc + 1 < kc1) chunk(kc + 1, std::integral_constant<int, 1>{});
-            if (kc + 2 < kc1) chunk(kc + 2, std::integral_constant<int, 2>{});
+        for (int kc = cur.kc0; kc < cur.kc1; ++kc) {
+            const bool last = kc + 1 >= cur.kc1;
+            const Item& T = last ? nxt : cur;
+            const int tkc = last ? nxt.kc0 : kc + 1;
+            sub(kc, T, tkc, std::integral_constant<int, 0>{});
+            sub(kc, T, tkc, std::integral_constant<int, 1>{});
+            sub(kc, T, tkc, std::integral_constant<int, 2>{});
+            sub(kc, T, tkc, std::integral_constant<int, 3>{});
         }
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        // every wave is past the last sub-stage's reads of V slot 1 and its V stores are done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
 
@@ -318,78 +320,106 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         // Y[py][1] = s[1] - (s[2] + s[3]); the partner wave (same wm, wn) supplies the other half.
         float y0v[16], y1v[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float sp[2][2];                              // [py][jj]
+        for (int rd = 0; rd < 4; ++rd) {
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                sp[0][jj] = acc[0 * 2 + jj][r] + acc[1 * 2 + jj][r] + acc[2 * 2 + jj][r];
-                sp[1][jj] = acc[1 * 2 + jj][r] - acc[2 * 2 + jj][r] - acc[3 * 2 + jj][r];
-            }
-            if (wx == 0) {       // j = 0, 1: keeps row 0 as (s0 + s1, s1), sends row 1 likewise
-                y0v[r] = sp[0][0] + sp[0][1];
-                y1v[r] = sp[0][1];
-                xs[r * 64 + lane] = sp[1][0] + sp[1][1];
-                xs[(16 + r) * 64 + lane] = sp[1][1];
-            } else {             // j = 2, 3: keeps row 1 as (s2, s2 + s3), sends row 0 likewise
-                y0v[r] = sp[1][0];
-                y1v[r] = sp[1][0] + sp[1][1];
-                xs[r * 64 + lane] = sp[0][0];
-                xs[(16 + r) * 64 + lane] = sp[0][0] + sp[0][1];
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (wx == 0) {
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int r = rd * 4 + r4;
+                float sp[2][2];                          // [py][jj]
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                y0v[r] = y0v[r] + xr[r * 64 + lane];
-                y1v[r] = y1v[r] - xr[(16 + r) * 64 + lane];
+                for (int jj = 0; jj < 2; ++jj) {
+                    sp[0][jj] = acc[0 * 2 + jj][r] + acc[1 * 2 + jj][r] + acc[2 * 2 + jj][r];
+                    sp[1][jj] = acc[1 * 2 + jj][r] - acc[2 * 2 + jj][r] - acc[3 * 2 + jj][r];
+                }
+                if (wx == 0) {   // j = 0, 1: keeps row 0 as (s0 + s1, s1), sends row 1 likewise
+                    y0v[r] = sp[0][0] + sp[0][1];
+                    y1v[r] = sp[0][1];
+                    xs[r4 * 64 + lane] = sp[1][0] + sp[1][1];
+                    xs[(4 + r4) * 64 + lane] = sp[1][1];
+                } else {         // j = 2, 3: keeps row 1 as (s2, s2 + s3), sends row 0 likewise
+                    y0v[r] = sp[1][0];
+                    y1v[r] = sp[1][0] + sp[1][1];
+                    xs[r4 * 64 + lane] = sp[0][0];
+                    xs[(4 + r4) * 64 + lane] = sp[0][0] + sp[0][1];
+                }
             }
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                y0v[r] = xr[r * 64 + lane] + y0v[r];
-                y1v[r] = xr[(16 + r) * 64 + lane] - y1v[r];
-            }
-        }
-        const int e_kz = kz, e_m = m_blk + 32 * wm + (lane & 31), e_n = n_blk + 32 * wn + 4 * (lane >> 5);
-        const int next = it + step;
-        const bool has_next = PERSIST && next < end;
-        if (has_next) {
-            // every wave's exchange reads are done before the next item's U lands in its slots
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            decode(next);
-            prologue();
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int r = rd * 4 + r4;
+                const float o0 = xr[r4 * 64 + lane], o1 = xr[(4 + r4) * 64 + lane];
+                if (wx == 0) {
+                    y0v[r] = y0v[r] + o0;
+                    y1v[r] = y1v[r] - o1;
+                } else {
+                    y0v[r] = o0 + y0v[r];
+                    y1v[r] = o1 - y1v[r];
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
         }
+        const int e_m = cur.m_blk + 32 * wm + (lane & 31), e_n = cur.n_blk + 32 * wn + 4 * (lane >> 5);
         if (e_m < w.tiles) {
             const int t2 = fdiv(e_m, w.dTw);
             const int tx = e_m - t2 * (p.Wo >> 1);
             const int b = fdiv(t2, w.dTh);
             const int ty = t2 - b * (p.Ho >> 1);
             const long long pix0 = ((long long)b * p.Ho + 2 * ty + wx) * p.Wo + 2 * tx;
+            if (p.ksplit == 1) {
+                // igemm's float4 epilogue (epi_store4) for the lane's two pixels, with the row
+                // offsets of both destinations formed once
+                const int n1 = p.N - p.n0;
+                const long long r0 = pix0 * p.n0, r1 = pix0 * n1;
+                const bool relu = p.flags & PU_EPI_RELU, accum = p.flags & PU_EPI_ACCUM;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = e_n + 8 * g;
-                const f32x4 y0 = {y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]};
-                const f32x4 y1 = {y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]};
-                if (p.ksplit == 1) {
-                    epi_store4(p, EpiRow{pix0, 0, 0}, n, y0);
-                    epi_store4(p, EpiRow{pix0 + 1, 0, 0}, n, y1);
-                } else {
-                    float* part = p.part + (long long)e_kz * p.M * p.N;
-                    *reinterpret_cast<f32x4*>(part + pix0 * p.N + n) = y0;
-                    *reinterpret_cast<f32x4*>(part + (pix0 + 1) * p.N + n) = y1;
+                for (int g = 0; g < 4; ++g) {
+                    const int n = e_n + 8 * g;
+                    const bool first = n < p.n0;
+                    float* dst = first ? p.dst0 : p.dst1;
+                    const float* msk = first ? p.mask0 : p.mask1;
+                    const int ld = first ? p.n0 : n1;
+                    const long long o0 = first ? r0 + n : r1 + (n - p.n0);
+                    f32x4 y[2] = {{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]},
+                                  {y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]}};
+                    const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) {
+                        const long long off = o0 + o * ld;
+                        f32x4 v = y[o];
+                        if (p.bias) v += bv;
+                        if (p.resid) v += *reinterpret_cast<const f32x4*>(p.resid + off);
+                        if (relu) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                        }
+                        if (msk) {
+                            const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
+                        }
+                        if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
+                        *reinterpret_cast<f32x4*>(dst + off) = v;
+                    }
+                }
+            } else {
+                float* part = p.part + (long long)cur.kz * p.M * p.N + pix0 * p.N + e_n;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    *reinterpret_cast<f32x4*>(part + 8 * g) = f32x4{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]};
+                    *reinterpret_cast<f32x4*>(part + p.N + 8 * g) = f32x4{y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]};
                 }
             }
         }
-        if (!has_next) break;
-        it = next;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        make_v(I0{}, ldv0);
+        if (!nxt.live) break;
+        it += step;
+        cur = nxt;
+        decode(it + step, nxt);
     }
+    // the stream's trailing (empty-range) LDS-DMA lands before the block's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // U = G g G^T per (n, 8 consecutive c), fp64 then rounded to fp32 and split into hi/mid/lo bf16:
