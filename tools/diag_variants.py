@@ -1,0 +1,30 @@
+"""Per-parameter gradient error of UNetp(batch_norm, bilinear) vs the reference golden, for the
+current dispatch switches (PU_WINO / PU_SMALLX6 from the environment)."""
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "plastic-unet_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np
+import torch
+from unet import UNetp
+from punet import bce_loss
+from conftest import golden
+
+DEV = torch.device("cuda")
+for tag, bn, bil in [("bn_bilinear", True, True), ("bn", True, False)]:
+    g = golden("unetp_%s.npz" % tag)
+    net = UNetp(1, 1, DEV, rule="oja", nbf=64, batch_norm=bn, bilinear_upsample=bil)
+    net.load_state_dict({k[2:]: torch.from_numpy(np.asarray(v)) for k, v in g.items() if k.startswith("p.")})
+    net.train()
+    xs = torch.from_numpy(np.asarray(g["xs"])).to(DEV)
+    y, hn = net(xs[0], torch.from_numpy(np.asarray(g["hebb"])).to(DEV))
+    loss = bce_loss(y, torch.from_numpy(np.asarray(g["t"])).to(DEV))
+    loss.backward()
+    print(tag, "Y err", (y.cpu() - torch.from_numpy(np.asarray(g["Y"])).reshape(y.shape)).abs().max().item())
+    for k, p in net.named_parameters():
+        if p.grad is None:
+            continue
+        ref = torch.from_numpy(np.asarray(g["g." + k])).reshape(p.grad.shape)
+        err = (p.grad.cpu() - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+        print("  %-28s %-16s rel-to-max %.2e" % (k, tuple(p.shape), err))
