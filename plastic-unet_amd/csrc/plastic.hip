@@ -164,7 +164,11 @@ __global__ void trace_kernel_v4(const float* __restrict__ H, const float* __rest
 //     chain in the same k order (== the MFMA's, bitwise), so every block holds row 0's Y;
 //  3. Y = sigmoid, X rows written out (the backward's input);
 //  4. H'[k][j] for the block's rows k from H, x0[k], y0[j] (unet_p.py:81-86 operation order).
-constexpr int FH_R = 16;      // rows per block
+#ifndef PU_FH_R
+#define PU_FH_R 16
+#endif
+constexpr int FH_R = PU_FH_R; // rows per block (8: rows 8..15 of the 16-row MFMA tiles are discarded)
+static_assert(FH_R == 8 || FH_R == 16, "rows per block");
 constexpr int FH_NT = 512;    // threads per block (2 blocks per CU at nbf 128: one block's feature
                                // loads overlap the other's GEMM / trace phases)
 constexpr int FH_WAVES = FH_NT / 64;
@@ -328,10 +332,12 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
         const int tile = wave + FH_WAVES * t;
         if (tile < tiles) {
             const int j = tile * 16 + (l & 15);
+            if (4 * (l >> 4) < FH_R) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int gi = i0 + 4 * (l >> 4) + r;
-                Y[((long long)b * N + gi) * N + j] = 1.f / (1.f + expf(-acc[t][r]));
+                for (int r = 0; r < 4; ++r) {
+                    const int gi = i0 + 4 * (l >> 4) + r;
+                    Y[((long long)b * N + gi) * N + j] = 1.f / (1.f + expf(-acc[t][r]));
+                }
             }
         }
     }

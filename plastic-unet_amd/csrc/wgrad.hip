@@ -832,17 +832,36 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(const WgradParams p) {
 // block's partial goes to slab row [block][n][tap*C + c] (bias at column K) and the fixed-order
 // fp64 split reduction below finishes it - deterministic like the GEMM path.
 constexpr int SW_TH = 16, SW_TW = 32;
+#ifndef PU_SW_ROW
+#define PU_SW_ROW 1     // 1: an item is a row of 3 taps over 4-pixel quads; 0: one tap per pixel
+#endif
+
+// 4x4 outer-product accumulate of 4 output channels g (x) 4 input channels x: channel pairs on
+// v_pk_fma_f32 (one rounding per element, as fmaf)
+__device__ __forceinline__ void sw_fma44(wg_f32x2 (&a)[4][2], const f32x4& g, const f32x4& x) {
+    const wg_f32x2 xa = {x[0], x[1]}, xb = {x[2], x[3]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const wg_f32x2 gg = {g[i], g[i]};
+        a[i][0] = __builtin_elementwise_fma(gg, xa, a[i][0]);
+        a[i][1] = __builtin_elementwise_fma(gg, xb, a[i][1]);
+    }
+}
 
 template <int C, int N>
 __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
     constexpr int HH = SW_TH + 2, HWD = SW_TW + 2;
     constexpr int CP = (C + 3) & ~3, C4 = CP / 4, N4 = N / 4;
-    constexpr int WITEMS = 9 * N4 * C4;
+    // weight items: (tap row r, 4 output x 4 input channels) with the 3 taps of the row, or
+    // (tap, 4 x 4) - plus bias items (4 output channels)
+    constexpr int RT = PU_SW_ROW ? 3 : 1;                 // taps per item
+    constexpr int WITEMS = (9 / RT) * N4 * C4;
     constexpr int ITEMS = WITEMS + N4;
     constexpr int GROUPS = 256 / ITEMS;
     static_assert(GROUPS >= 1, "items");
+    constexpr int ACC = RT * 16;
     constexpr int HALO = HH * HWD * CP, GT = SW_TH * SW_TW * N;
-    constexpr int SMEM = (HALO + GT) > (GROUPS * ITEMS * 16) ? (HALO + GT) : (GROUPS * ITEMS * 16);
+    constexpr int SMEM = (HALO + GT) > (GROUPS * ITEMS * ACC) ? (HALO + GT) : (GROUPS * ITEMS * ACC);
     __shared__ __attribute__((aligned(16))) float smem[SMEM];
     float* halo = smem;
     float* gt = smem + HALO;
@@ -851,21 +870,21 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
     const int item = tid % ITEMS, grp = tid / ITEMS;
     const bool active = grp < GROUPS;
     const bool wi = item < WITEMS;
-    int tap = 0, co4 = 0, ci4 = 0;
+    int tq = 0, co4 = 0, ci4 = 0;                          // tq: tap row (RT = 3) or tap
     if (wi) {
-        tap = item / (N4 * C4);
-        const int rem = item - tap * (N4 * C4);
+        tq = item / (N4 * C4);
+        const int rem = item - tq * (N4 * C4);
         co4 = rem / C4;
         ci4 = rem - co4 * C4;
     } else {
         co4 = item - WITEMS;
     }
-    const int tr = tap / 3, ts = tap - tr * 3;
-    float acc[4][4];
+    const int tr = RT == 3 ? tq : tq / 3, ts = RT == 3 ? 0 : tq - tr * 3;
+    wg_f32x2 acc[RT][4][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+        for (int i = 0; i < 4; ++i) acc[t][i][0] = acc[t][i][1] = wg_f32x2{0.f, 0.f};
 
     const int ntiles = p.batch * p.tiles_h * p.tiles_w;
     // the tile's halo and gradient rows are loaded into registers one tile ahead (all loads of a
@@ -930,21 +949,45 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
         if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
         __syncthreads();
         if (active) {
-            if (wi) {
+            if (RT == 3) {
+                // 4 consecutive output pixels x the row's 3 taps: 4 gradient + 6 halo reads per
+                // 192 fmas (the per-tap form: 2 reads per 16)
+                constexpr int QW = SW_TW / 4;
+                for (int pq = grp; pq < SW_TH * QW; pq += GROUPS) {
+                    const int row = pq / QW, col0 = (pq - row * QW) * 4;
+                    f32x4 g[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        g[u] = *reinterpret_cast<const f32x4*>(gt + (row * SW_TW + col0 + u) * N + 4 * co4);
+                    if (wi) {
+                        f32x4 x[6];
+#pragma unroll
+                        for (int v = 0; v < 6; ++v)
+                            x[v] = *reinterpret_cast<const f32x4*>(halo + ((row + tr) * HWD + col0 + v) * CP + 4 * ci4);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+#pragma unroll
+                            for (int s3 = 0; s3 < RT; ++s3) sw_fma44(acc[s3], g[u], x[u + s3]);
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            acc[0][0][0] += wg_f32x2{g[u][0], g[u][1]};
+                            acc[0][0][1] += wg_f32x2{g[u][2], g[u][3]};
+                        }
+                    }
+                }
+            } else if (wi) {
                 for (int pp = grp; pp < SW_TH * SW_TW; pp += GROUPS) {
                     const int row = pp / SW_TW, col = pp - row * SW_TW;
                     const f32x4 g4 = *reinterpret_cast<const f32x4*>(gt + pp * N + 4 * co4);
                     const f32x4 x4 = *reinterpret_cast<const f32x4*>(halo + ((row + tr) * HWD + col + ts) * CP + 4 * ci4);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(g4[i], x4[j], acc[i][j]);
+                    sw_fma44(acc[0], g4, x4);
                 }
             } else {
                 for (int pp = grp; pp < SW_TH * SW_TW; pp += GROUPS) {
                     const f32x4 g4 = *reinterpret_cast<const f32x4*>(gt + pp * N + 4 * co4);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[0][i] += g4[i];
+                    acc[0][0][0] += wg_f32x2{g4[0], g4[1]};
+                    acc[0][0][1] += wg_f32x2{g4[2], g4[3]};
                 }
             }
         }
@@ -953,30 +996,39 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
     __syncthreads();
     if (active) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) smem[(grp * ITEMS + item) * 16 + i * 4 + j] = acc[i][j];
-    }
-    __syncthreads();
-    if (tid < ITEMS) {
-        float v[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) v[e] = 0.f;
-        for (int g = 0; g < GROUPS; ++g)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) v[e] += smem[(g * ITEMS + tid) * 16 + e];
-        float* slab = p.slab + (long long)blockIdx.x * p.Nr * p.Kcp;
-        if (tid < WITEMS) {
+        for (int t = 0; t < RT; ++t)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int c = 4 * ci4 + j;
-                    if (c < C) slab[(long long)(4 * co4 + i) * p.Kcp + tap * C + c] = v[i * 4 + j];
+                for (int h = 0; h < 2; ++h) {
+                    smem[(grp * ITEMS + item) * ACC + t * 16 + i * 4 + 2 * h] = acc[t][i][h][0];
+                    smem[(grp * ITEMS + item) * ACC + t * 16 + i * 4 + 2 * h + 1] = acc[t][i][h][1];
                 }
-        } else {
+    }
+    __syncthreads();
+    if (tid < ITEMS) {
+        float* slab = p.slab + (long long)blockIdx.x * p.Nr * p.Kcp;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) slab[(long long)(4 * co4 + i) * p.Kcp + p.K] = v[i];
+        for (int t = 0; t < RT; ++t) {
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) v[e] = 0.f;
+            for (int g = 0; g < GROUPS; ++g)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) v[e] += smem[(g * ITEMS + tid) * ACC + t * 16 + e];
+            if (tid < WITEMS) {
+                const int tap = RT == 3 ? 3 * tr + t : tq;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int c = 4 * ci4 + j;
+                        if (c < C) slab[(long long)(4 * co4 + i) * p.Kcp + tap * C + c] = v[i * 4 + j];
+                    }
+            } else if (t == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) slab[(long long)(4 * co4 + i) * p.Kcp + p.K] = v[i];
+            }
         }
     }
 }
@@ -1135,7 +1187,8 @@ static bool small_wgrad_ok(const pu_wgrad_args* a) {
            (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
 }
 
-// Measured alternatives (round 1): 64 x 576 6-wave tiles for the 64-channel layers (-6 %), a
+// Measured alternatives: capping the GEMM-path split count at 2 / 4 (round 3: C2 4060 -> 2262 /
+// 2968 img/s - the deep layers' slab traffic is cheaper than idle CUs); round 1: 64 x 576 6-wave tiles for the 64-channel layers (-6 %), a
 // 3-wave 64 x 192 tile (-8 %), a split-once-planes kernel that still staged fp32 through LDS
 // (-10...-25 %); the halo kernel below replaced all of them on 3x3/s1 layers.
 static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {

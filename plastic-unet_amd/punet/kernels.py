@@ -62,7 +62,7 @@ _WINO = os.environ.get("PU_WINO", "1") != "0"
 
 # fp32 8/16-channel 3x3 convolutions on the 16x16x32 MFMA kernel (csrc/smallconv.hip) or the VALU
 # direct kernel (PU_SMALLX6=0; tests flip it with set_smallx6)
-_SMALLX6 = os.environ.get("PU_SMALLX6", "0") != "0"
+_SMALLX6 = os.environ.get("PU_SMALLX6", "1") != "0"
 
 
 def set_smallx6(on):

@@ -5,10 +5,11 @@ set -u
 VAR=$1; VALS=$2; shift 2
 for rep in 1 2; do
   for v in $VALS; do
-    mkdir -p gpurun_out/ab; env $VAR=$v timeout -k 10 240 python bench.py --no-cpu-baseline --no-oja "$@" > gpurun_out/ab/$VAR.$v.log 2>&1 || { echo "bench failed ($VAR=$v)"; tail -20 gpurun_out/ab/$VAR.$v.log; exit 1; }
-    out=$(grep "^{\"metric\"" gpurun_out/ab/$VAR.$v.log | tail -1)
+    log=gpurun_out/ab/$VAR.$(basename $v).log
+    mkdir -p gpurun_out/ab; env $VAR=$v timeout -k 10 240 python bench.py --no-cpu-baseline --no-oja "$@" > $log 2>&1 || { echo "bench failed ($VAR=$v)"; tail -20 $log; exit 1; }
+    out=$(grep "^{\"metric\"" $log | tail -1)
     python -c "
 import json,sys; d=json.loads(sys.argv[1]); r=d['roofline']
-print('$VAR=$v', d['value'], 'img/s', d['ms_per_step'], 'ms', r['kernel'], r['frac'], r.get('direct_equivalent_frac'))" "$out"
+print('$VAR=$(basename $v)', d['value'], 'img/s', d['ms_per_step'], 'ms', r['kernel'], r['frac'], r.get('direct_equivalent_frac'))" "$out"
   done
 done
