@@ -232,25 +232,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
         const int lane = tid % L;
         constexpr int PPP = FH_NT / L;          // pixels per pass
         const int npix = (fuse ? FH_R + 1 : FH_R) * N;
-        for (int q0 = tid / L; q0 < npix; q0 += U * PPP) {
-            const T* px[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int q = min(q0 + u * PPP, npix - 1);
-                const int r = (int)fdiv((unsigned)q, dN), k = q - r * N;
-                px[u] = fb + ((long long)(r < FH_R ? i0 + r : 0) * N + k) * C;
-            }
-            float s[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) s[u] = 0.f;
-            for (int c = lane * 4; c < C; c += 4 * L) {
-                const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + c);
-                f32x4 v[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) v[u] = fh_ld4<T>(px[u] + c);
-#pragma unroll
-                for (int u = 0; u < U; ++u) s[u] += dot4_fma(v[u], ww);
-            }
+        auto reduce_store = [&](int q0, float (&s)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 float t = s[u];
@@ -261,6 +243,28 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
                 const int q = q0 + u * PPP;
                 if (lane == 0 && q < npix) xs[q] = t + bias;
             }
+        };
+        auto pixel = [&](int q) -> const T* {
+            q = min(q, npix - 1);
+            const int r = (int)fdiv((unsigned)q, dN), k = q - r * N;
+            return fb + ((long long)(r < FH_R ? i0 + r : 0) * N + k) * C;
+        };
+        for (int q0 = tid / L; q0 < npix; q0 += U * PPP) {
+            const T* px[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) px[u] = pixel(q0 + u * PPP);
+            float sacc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) sacc[u] = 0.f;
+            for (int c = lane * 4; c < C; c += 4 * L) {
+                const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + c);
+                f32x4 v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) v[u] = fh_ld4<T>(px[u] + c);
+#pragma unroll
+                for (int u = 0; u < U; ++u) sacc[u] += dot4_fma(v[u], ww);
+            }
+            reduce_store(q0, sacc);
         }
     }
     __syncthreads();
@@ -313,13 +317,32 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
             if (tile < tiles) {
                 const float* wcol = ws + (l >> 4) * N + tile * 16 + (l & 15);
                 const float* xrow = xs + (l & 15) * N + k0 + (l >> 4);
-                for (int kk = 0; kk < kc; kk += 4)
+                // operands of 4 k-steps read before their MFMAs (kc % 16 == 0 or kc = 4 .. 12: see
+                // fused_head_chunk - the tail loop takes the rest)
+                int kk = 0;
+                for (; kk + 16 <= kc; kk += 16) {
+                    float xa[4], wb[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) { xa[j] = xrow[kk + 4 * j]; wb[j] = wcol[(kk + 4 * j) * N]; }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[j], wb[j], acc[t], 0, 0, 0);
+                }
+                for (; kk < kc; kk += 4)
                     acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xrow[kk], wcol[kk * N], acc[t], 0, 0, 0);
             }
         }
         if (fuse && tid < N && PU_FH_ABL != 2) {
+            // the same k-ordered fmaf chain; 8 k's operands read ahead of their fmas
             float s0 = acc0;
-            for (int kk = 0; kk < kc; ++kk) s0 = fmaf(xs[FH_R * N + k0 + kk], ws[kk * N + tid], s0);
+            int kk = 0;
+            for (; kk + 8 <= kc; kk += 8) {
+                float xa[8], wb[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) { xa[j] = xs[FH_R * N + k0 + kk + j]; wb[j] = ws[(kk + j) * N + tid]; }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s0 = fmaf(xa[j], wb[j], s0);
+            }
+            for (; kk < kc; ++kk) s0 = fmaf(xs[FH_R * N + k0 + kk], ws[kk * N + tid], s0);
             acc0 = s0;
         }
         __syncthreads();

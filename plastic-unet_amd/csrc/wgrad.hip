@@ -1694,6 +1694,59 @@ __global__ __launch_bounds__(256 * NT) void wgrad_halo_bf16_kernel(const WgradBf
     }
 }
 
+// One-launch reduction for the direct small-channel / stem weight gradients: up to 1024 split
+// rows of a few thousand entries, where the two-pass form's per-thread chains over 64 splits were
+// latency rounds, not bytes.  Block = 16 entries (4 float4 quads) x 64 split lanes: lane s sums
+// splits s, s + 64, ... in 4 fp64 chains, then thread e < 16 sums the 64 lanes in order and
+// scatters entry e into [n][c][kh][kw] (bias at column K) - a fixed order, deterministic.
+constexpr int WR_E = 16, WR_S = 64;
+__global__ __launch_bounds__(256) void wgrad_reduce_wide_kernel(const float* __restrict__ slab, int splits,
+                                                                 long long total, int N, int Kcp, int K, int C,
+                                                                 int kh, int kw, int bias_mode, float* __restrict__ dw,
+                                                                 float* __restrict__ db, int accumulate) {
+    __shared__ double part[WR_S][WR_E];
+    const int quad = threadIdx.x & 3, sl = threadIdx.x >> 2;
+    const long long idx0 = (long long)blockIdx.x * WR_E + 4 * quad;
+    double a[4][4] = {};
+    if (idx0 < total) {                               // total % 4 == 0 (Kcp % 4 == 0)
+        const float* sp = slab + idx0;
+        int z = sl;
+        for (; z + 3 * WR_S < splits; z += 4 * WR_S) {
+            f32x4 v[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const f32x4*>(sp + (long long)(z + c * WR_S) * total);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a[c][e] += (double)v[c][e];
+        }
+        for (; z < splits; z += WR_S) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(sp + (long long)z * total);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[0][e] += (double)v[e];
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[sl][4 * quad + e] = (a[0][e] + a[1][e]) + (a[2][e] + a[3][e]);
+    __syncthreads();
+    if (threadIdx.x >= WR_E) return;
+    const long long idx = (long long)blockIdx.x * WR_E + threadIdx.x;
+    if (idx >= total) return;
+    double sum = 0.0;
+    for (int l = 0; l < WR_S; ++l) sum += part[l][threadIdx.x];
+    const float v = (float)sum;
+    const int n = (int)(idx / Kcp), k = (int)(idx - (long long)n * Kcp);
+    if (n >= N) return;
+    if (k < K) {
+        const int tap = k / C, ch = k - tap * C;
+        const int r = tap / kw, ss = tap - r * kw;
+        float* o = dw + (((long long)n * C + ch) * kh + r) * kw + ss;
+        *o = accumulate ? *o + v : v;
+    } else if (bias_mode == 1 && k == K) {
+        db[n] = accumulate ? db[n] + v : v;
+    }
+}
+
 // phase 2 of every weight-gradient path: fixed-order fp64 reduction of the split partials and
 // the scatter into PyTorch's [n][c][kh][kw] (+ bias)
 static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* workspace, hipStream_t s) {
@@ -1701,6 +1754,12 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
     const dim3 fgrid((unsigned)((threads + 255) / 256));
     const int taps = a->kh * a->kw;
+    if ((pl.small || pl.stem) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
+        hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)ceil_div(total, (long long)WR_E)), dim3(256), 0, s,
+                           (const float*)workspace, pl.splits, total, a->n, pl.Kcp, pl.K, pl.C, a->kh, a->kw,
+                           a->bias_mode, a->dweight, a->dbias, a->accumulate);
+        return check_launch("pu_wgrad (reduce)");
+    }
     if (a->bias_mode != 2 && taps <= 9 && pl.C % 4 == 0 && pl.Kcp % 4 == 0 && ((uintptr_t)a->dweight & 15) == 0) {
         const dim3 tgrid((unsigned)ceil_div(pl.C, 256), (unsigned)a->n);
         const dim3 tblock((unsigned)(64 * taps));
