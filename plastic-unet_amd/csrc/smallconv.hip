@@ -27,8 +27,11 @@ constexpr int SX_HP = SX_HH * SX_HW;                  // halo pixels (612)
 typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
 typedef float f32x4s __attribute__((ext_vector_type(4)));
 
+// LDS allows 4-5 / 2 blocks per CU (29 / 59 KB): waves_per_eu(4 / 2) lets the compiler use 128 / 256
+// registers instead of squeezing into 64 with the accumulators parked in AGPRs (320 accvgpr moves
+// per wave at C = 8)
 template <int C, int N>
-__global__ __launch_bounds__(256) void smallconv_x6_kernel(const IgemmParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 8 ? 4 : 2))) void smallconv_x6_kernel(const IgemmParams p) {
 #pragma clang fp contract(off)
     constexpr int HALVES = C / 8;                   // 8-channel LDS images per plane
     constexpr int KS = (9 * C + 31) / 32;           // 32-wide k steps
@@ -123,12 +126,11 @@ __global__ __launch_bounds__(256) void smallconv_x6_kernel(const IgemmParams p) 
         for (int t = 0; t < 8; ++t) {
             const int row = 4 * wave + (t >> 1), col = (t & 1) * 16 + j;
             const int hp = (row + r) * SX_HW + col + sx;
+            // k past 9C (tap >= 9) reads tap 0's window: finite values against zero weight planes
             bf16x8s xb[3];
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
+            for (int pl = 0; pl < 3; ++pl)
                 xb[pl] = *reinterpret_cast<const bf16x8s*>(img + ((pl * HALVES + c8) * SX_HP + hp) * 8);
-                if (!live) xb[pl] = bf16x8s{};
-            }
             f32x4s c = acc[t];
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][1], xb[1], c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][2], xb[0], c, 0, 0, 0);
