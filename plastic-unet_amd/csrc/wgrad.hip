@@ -857,18 +857,24 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
     constexpr int RT = PU_SW_ROW ? 3 : 1;                 // taps per item
     constexpr int WITEMS = (9 / RT) * N4 * C4;
     constexpr int ITEMS = WITEMS + N4;
-    constexpr int GROUPS = 256 / ITEMS;
+    // LDS bank conflicts (64 banks: a ds_read_b128 serves 16 lanes per cycle): a group's items
+    // padded to a multiple of 16 lanes keeps each 16-lane phase inside one pixel group, and a
+    // halo row pitch of HWD + 1 pixels puts the 3 tap rows x input-channel quads on distinct banks
+    // (C = 8: chunk offsets {0,1,6,7,12,13}; C = 16: {0..3, 12..15, 8..11})
+    constexpr int ITEMS_P = ITEMS >= 12 ? (ITEMS + 15) / 16 * 16 : ITEMS;
+    constexpr int HWP = HWD + 1;
+    constexpr int GROUPS = 256 / ITEMS_P;
     static_assert(GROUPS >= 1, "items");
     constexpr int ACC = RT * 16;
-    constexpr int HALO = HH * HWD * CP, GT = SW_TH * SW_TW * N;
+    constexpr int HALO = HH * HWP * CP, GT = SW_TH * SW_TW * N;
     constexpr int SMEM = (HALO + GT) > (GROUPS * ITEMS * ACC) ? (HALO + GT) : (GROUPS * ITEMS * ACC);
     __shared__ __attribute__((aligned(16))) float smem[SMEM];
     float* halo = smem;
     float* gt = smem + HALO;
 
     const int tid = threadIdx.x;
-    const int item = tid % ITEMS, grp = tid / ITEMS;
-    const bool active = grp < GROUPS;
+    const int item = tid % ITEMS_P, grp = tid / ITEMS_P;
+    const bool active = grp < GROUPS && item < ITEMS;
     const bool wi = item < WITEMS;
     int tq = 0, co4 = 0, ci4 = 0;                          // tq: tap row (RT = 3) or tap
     if (wi) {
@@ -939,7 +945,10 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
 #pragma unroll
         for (int it = 0; it < PH; ++it) {
             const int e = it * 256 + tid;
-            if (e < NH) *reinterpret_cast<f32x4*>(halo + (e / C4) * CP + 4 * (e % C4)) = rh[it];
+            if (e < NH) {
+                const int pix = e / C4, hy = pix / HWD, hx = pix - hy * HWD;
+                *reinterpret_cast<f32x4*>(halo + (hy * HWP + hx) * CP + 4 * (e % C4)) = rh[it];
+            }
         }
 #pragma unroll
         for (int it = 0; it < PG2; ++it) {
@@ -963,7 +972,7 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
                         f32x4 x[6];
 #pragma unroll
                         for (int v = 0; v < 6; ++v)
-                            x[v] = *reinterpret_cast<const f32x4*>(halo + ((row + tr) * HWD + col0 + v) * CP + 4 * ci4);
+                            x[v] = *reinterpret_cast<const f32x4*>(halo + ((row + tr) * HWP + col0 + v) * CP + 4 * ci4);
 #pragma unroll
                         for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -980,7 +989,7 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
                 for (int pp = grp; pp < SW_TH * SW_TW; pp += GROUPS) {
                     const int row = pp / SW_TW, col = pp - row * SW_TW;
                     const f32x4 g4 = *reinterpret_cast<const f32x4*>(gt + pp * N + 4 * co4);
-                    const f32x4 x4 = *reinterpret_cast<const f32x4*>(halo + ((row + tr) * HWD + col + ts) * CP + 4 * ci4);
+                    const f32x4 x4 = *reinterpret_cast<const f32x4*>(halo + ((row + tr) * HWP + col + ts) * CP + 4 * ci4);
                     sw_fma44(acc[0], g4, x4);
                 }
             } else {

@@ -63,6 +63,8 @@ CONV_CASES = [
     (1, 16, 48, 64, 128, 192),  # halo2 wgrad (64-channel tiles): 3 input x 3 output tiles, 3 stages per row
     (2, 37, 45, 16, 0, 16),     # small-channel direct kernels: several 16x32 tiles, ragged edges
     (1, 19, 70, 4, 4, 4),       # small-channel, two 4-channel sources, N = 4
+    (1, 20, 36, 8, 4, 8),       # small-channel wgrad C = 12 (padded item groups), N = 8
+    (2, 16, 40, 4, 0, 16),      # small-channel wgrad C = 4, N = 16
     (2, 32, 64, 32, 0, 32),     # 32-channel lean tile (128 x 32): fwd and dgrad, N = 32
     (1, 16, 64, 32, 32, 32),    # 32-channel lean tile, two sources
     (32, 64, 64, 32, 0, 32),    # 256 x 32 lean tile (>= 480 tiles), the C4 64^2 level
