@@ -95,12 +95,14 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
 /* PU_CONV_NO_HALO: a dispatch hint, not an epilogue flag - keep a bf16 3x3/s1 layer that the halo
  * kernel would take (width 32/64/128) on the per-tap lean kernel (A/B runs and the bit-identity
  * test: both compute the same sums in the same order when the per-tap launch is not split) */
-/* PU_CONV_HALO_V1: a dispatch hint - take the register-staged 256-pixel halo kernel instead of the
- * DMA-ring 512-pixel one (A/B runs; the per-tap bit-identity test) */
+/* PU_CONV_HALO_DMA: a dispatch hint - take the DMA-ring 512-pixel halo kernel instead of the
+ * register-staged 256-pixel one (the default); its sums differ from the per-tap kernel's by at most
+ * one bf16 ulp of the output (A/B runs).  PU_CONV_HALO_V1 (the register-staged kernel) is the
+ * default and kept as an accepted no-op flag. */
 /* PU_CONV_NO_SMALLX6: a dispatch hint - keep an 8/16-channel 3x3 layer on the VALU direct kernel
  * instead of the 16x16x32 MFMA one (A/B runs) */
 enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8, PU_CONV_NO_HALO = 16,
-       PU_CONV_HALO_V1 = 32, PU_CONV_NO_SMALLX6 = 64 };
+       PU_CONV_HALO_V1 = 32, PU_CONV_NO_SMALLX6 = 64, PU_CONV_HALO_DMA = 128 };
 
 typedef struct {
     int batch;

@@ -1007,12 +1007,13 @@ static int device_cus_b() {
 }
 
 // the DMA-ring halo kernel: the halo kernel's shapes with 512-pixel row blocks (R = 512 / W rows);
-// PU_CONV_HALO_V1 keeps the register-staged kernel (A/B runs, its bit-identity test)
+// opt-in with PU_CONV_HALO_DMA (A/B runs, its bit-identity test); the default is the register-staged
+// kernel, which the Python host runs too
 static bool halo2_ok_b(const pu_conv_args* a) {
     // its epilogue stores 8 channels (16 B) per lane: 8-channel split point, 16-byte-aligned tensors
     const uintptr_t ae = (uintptr_t)a->dst0 | (uintptr_t)a->dst1 | (uintptr_t)a->mask0 | (uintptr_t)a->mask1 |
                          (uintptr_t)a->resid;
-    return halo_ok_b(a) && !(a->flags & PU_CONV_HALO_V1) && a->out_h % (512 / a->out_w) == 0 && a->n0 % 8 == 0 &&
+    return halo_ok_b(a) && (a->flags & PU_CONV_HALO_DMA) && a->out_h % (512 / a->out_w) == 0 && a->n0 % 8 == 0 &&
            (ae & 15) == 0;
 }
 

@@ -1034,7 +1034,7 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradParams p) {
                         const int c = 4 * ci4 + j;
                         if (c < C) slab[(long long)(4 * co4 + i) * p.Kcp + tap * C + c] = v[i * 4 + j];
                     }
-            } else if (t == 0) {
+            } else if (t == 0 && p.bias_mode == 1) {   // column K exists only with a bias (Kc = K + 1)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) slab[(long long)(4 * co4 + i) * p.Kcp + p.K] = v[i];
             }

@@ -10,7 +10,7 @@ import torch
 
 from . import _lib
 from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, WinoJob, check,
-                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1,
+                   PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1, PU_CONV_HALO_DMA,
                    PU_CONV_NO_SMALLX6)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
@@ -33,21 +33,24 @@ _FP32_MATH = os.environ.get("PU_FP32_MATH", "split6")
 
 
 # bf16 3x3/s1 convolutions of width 32/64/128: 2 = the DMA-ring halo kernel (512-pixel
-# row blocks), 1 = the register-staged halo kernel (default), 0 = the per-tap lean kernel (PU_CONV_HALO:
+# row blocks, PU_CONV_HALO_DMA), 1 = the register-staged halo kernel (default, as at the C-ABI),
+# 0 = the per-tap lean kernel (PU_CONV_HALO:
 # A/B runs; tests flip it with set_conv_halo)
 _CONV_HALO = int(os.environ.get("PU_CONV_HALO", "1"))
 
 
 def set_conv_halo(mode):
-    """Route eligible bf16 convolutions: 2 (or True) DMA-ring halo kernel, 1 register-staged halo
-    kernel, 0 (or False) per-tap kernel.  Returns the previous setting."""
+    """Route eligible bf16 convolutions: 2 DMA-ring halo kernel, 1 (or True) register-staged halo
+    kernel - the default, as at the C-ABI -, 0 (or False) per-tap kernel.  Returns the previous
+    setting."""
     global _CONV_HALO
-    prev, _CONV_HALO = _CONV_HALO, (2 if mode is True else 0 if mode is False else int(mode))
+    prev, _CONV_HALO = _CONV_HALO, (1 if mode is True else 0 if mode is False else int(mode))
     return prev
 
 
 def _halo_flags():
-    return {2: 0, 1: PU_CONV_HALO_V1}.get(_CONV_HALO, PU_CONV_NO_HALO)
+    # the C-ABI default (no flag) is the register-staged kernel; 2 opts in to the DMA ring
+    return {2: PU_CONV_HALO_DMA, 1: 0}.get(_CONV_HALO, PU_CONV_NO_HALO)
 
 
 def fp32_math():
@@ -341,7 +344,9 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
         check(fn(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, k_pad, cgroup, _stream()), "pu_pack_weight")
     if out.dtype == torch.float32 and _FP32_MATH == "split6" and k_pad % 16 == 0:
         out._split6 = split_weight6(out)      # travels with the packed operand (igemm picks it up)
-        if wino_wanted(w, mode):              # so does the Winograd operand of a 3x3 conv
+        # so does the Winograd operand of a 3x3 conv - only while Winograd dispatch is on, so a
+        # PU_WINO=0 run neither holds nor refreshes U (set_wino before packing to switch)
+        if _WINO and wino_wanted(w, mode):
             n, c = (d0, d1) if mode == 0 else (d1, d0)
             out._wino = torch.empty(lib().pu_wino_bytes(n, c) // 2, dtype=BF16, device=w.device)
             pack_wino([(w, out._wino, mode == 1)])

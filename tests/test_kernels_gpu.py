@@ -115,6 +115,28 @@ def test_conv3x3_fwd_dgrad_wgrad(B, H, W, c0, c1, cout):
     assert_close(db, br.grad)
 
 
+@pytest.mark.parametrize("C,N", [(4, 4), (8, 8), (12, 8), (16, 16)])
+def test_small_channel_wgrad_without_bias(C, N):
+    """The small-channel weight gradient with bias_mode 0 (K = 9C is then a multiple of 4, so the
+    slab has no bias column): every entry equals the bias_mode 1 run of the same layer - an
+    unguarded bias write at column K would land on the next row's tap-0 entry (and one float past
+    the slab for the last row of the last block)."""
+    g = torch.Generator().manual_seed(C * 10 + N)
+    B, H, W = 2, 24, 40
+    x = nhwc(rnd(B, C, H, W, g=g)).to(DEV)
+    dz = nhwc(rnd(B, N, H, W, g=g)).to(DEV)
+    dw0 = torch.full((N, C, 3, 3), float("nan"), device=DEV)
+    K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, rows=dz, n=N, src0=x, c0=C,
+            dweight=dw0, bias_mode=0)
+    dw1 = torch.empty(N, C, 3, 3, device=DEV)
+    db1 = torch.empty(N, device=DEV)
+    K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, rows=dz, n=N, src0=x, c0=C,
+            dweight=dw1, bias_mode=1, dbias=db1)
+    assert torch.equal(dw0, dw1)
+    ref = torch.nn.grad.conv2d_weight(nchw(x).cpu(), (N, C, 3, 3), nchw(dz).cpu(), padding=1)
+    assert_close(dw0, ref)
+
+
 @pytest.mark.parametrize("B,H,W,c0,c1,cout", SMALL_X6_CASES)
 def test_conv3x3_small_channel_x6(B, H, W, c0, c1, cout):
     prev = K.set_smallx6(True)

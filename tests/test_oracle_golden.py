@@ -217,13 +217,16 @@ def test_add_coords_closed_form():
     assert torch.allclose(out[1, 3, 0, 0], torch.tensor(np.sqrt(2 * 1.5 ** 2), dtype=torch.float32))
 
 
-@pytest.mark.parametrize("tag,bn,bil", [("bn", True, False), ("bilinear", False, True), ("bn_bilinear", True, True)])
+@pytest.mark.parametrize("tag,bn,bil", [("bn", True, False), ("bilinear", False, True), ("bn_bilinear", True, True),
+                                        ("bn_bilinear_m", True, True)])
 def test_unetp_variants_fixture(tag, bn, bil):
     """UNetp(batch_norm / bilinear_upsample): init RNG order, train-mode fwd/bwd, the running
-    statistics after two forwards, and the eval-mode forward (reference, unet_p.py:186-193, :235-236)."""
+    statistics after two forwards, and the eval-mode forward (reference, unet_p.py:186-193, :235-236).
+    bn_bilinear_m: the margin-certified 32x32 fixture (seed 500 + s for the init, see gen_golden.py)."""
     g = golden("unetp_%s.npz" % tag)
-    torch.manual_seed(5)
-    net = oracle.RefUNetp(1, 1, rule="oja", nbf=64, batch_norm=bn, bilinear_upsample=bil)
+    nbf = 32 if tag.endswith("_m") else 64
+    torch.manual_seed(500 + int(g["seed"]) if tag.endswith("_m") else 5)
+    net = oracle.RefUNetp(1, 1, rule="oja", nbf=nbf, batch_norm=bn, bilinear_upsample=bil)
     for k, v in net.state_dict().items():
         np.testing.assert_array_equal(v.numpy(), g["p." + k])
     net.train()
@@ -255,7 +258,7 @@ def test_unetp_variants_fixture(tag, bn, bil):
     assert nbuf == (3 * 18 if bn else 0)      # 18 BatchNorm2d layers x (mean, var, count)
     net.eval()
     with torch.no_grad():
-        ye, he = net(xs[2], torch.zeros(64, 64))
+        ye, he = net(xs[2], torch.zeros(nbf, nbf))
     close(ye, g["Ye"])
     close(he, g["He"])
 

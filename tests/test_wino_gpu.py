@@ -49,6 +49,10 @@ CASES = [
     (4, 8, 8, 512, 0, 512),       # split-K (bottom level shape): 64 tiles, 8 channel blocks
     (2, 16, 16, 256, 256, 256),   # split-K with two sources (the 16x16 up level)
     (1, 2, 2, 32, 0, 64),         # a single 2x2 tile
+    # > 256 items: the persistent kernel (items streamed per block, next-item prefetch during the
+    # epilogue, per-XCD item ranges)
+    (5, 128, 128, 64, 0, 64),     # 320 items, 40 per XCD
+    (3, 96, 80, 128, 0, 192),     # 270 items: ragged per-XCD ranges (270 % 8 = 6), 3 channel blocks
 ]
 
 
@@ -136,3 +140,40 @@ def test_pack_wino_is_G_g_Gt_split_exactly():
         got = planes.permute(1, 2, 3, 0, 4).reshape(16, 3, n, c)
         assert torch.equal(got[:, 0] + got[:, 1] + got[:, 2], U), dgrad
         assert torch.equal(got[:, 0], U.bfloat16().float())
+
+
+_PERSIST_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from punet import kernels as K, trunk as T
+B, H, W, C, N = 5, 128, 128, 64, 64
+g = torch.Generator().manual_seed(77)
+x = torch.randn(B, H, W, C, generator=g).relu().cuda()
+w = (torch.randn(N, C, 3, 3, generator=g) * 0.06).cuda()
+b = torch.randn(N, generator=g).cuda()
+dz = torch.randn(B, H, W, N, generator=g).cuda()
+pk = T._Packs()
+y = T.conv3x3(x, w, b, pk, relu=True)
+d0, _ = T.conv3x3_dgrad(dz, w, pk, mask0=x)
+torch.save({"y": y.cpu(), "d": d0.cpu()}, sys.argv[1])
+"""
+
+
+def test_wino_persistent_equals_one_item_per_block(tmp_path):
+    """The persistent kernel (320 items on 256 blocks) and the one-item-per-block launch
+    (PU_WINO_PERSIST=0, read once per process - hence two child processes) form the same per-item
+    sums in the same order: forward and data gradient bit-identical."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plastic-unet_amd")
+    out = {}
+    for persist in ("1", "0"):
+        f = str(tmp_path / ("p%s.pt" % persist))
+        env = dict(os.environ, PU_WINO_PERSIST=persist, PU_WINO="1")
+        r = subprocess.run([sys.executable, "-c", _PERSIST_SCRIPT, f, root], env=env, capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[persist] = torch.load(f, weights_only=True)
+    assert torch.equal(out["1"]["y"], out["0"]["y"])
+    assert torch.equal(out["1"]["d"], out["0"]["d"])
