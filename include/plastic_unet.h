@@ -190,7 +190,8 @@ typedef struct {
 } pu_wgrad_args;
 
 size_t pu_wgrad_workspace_bytes(const pu_wgrad_args* a);
-/* the tile (bn x bk), loader (qvec: 0 scalar, 1 float4, 2 small-channel direct kernel, 3 halo-reuse kernel) and
+/* the tile (bn x bk), loader (qvec: 0 scalar, 1 float4, 2 small-channel direct kernel, 3 halo-reuse kernel,
+ * 4 stem kernel, 5 Winograd-domain kernel) and
  * pixel-row split count pu_wgrad would use */
 int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec, int* splits);
 int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);

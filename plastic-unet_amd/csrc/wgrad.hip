@@ -754,6 +754,374 @@ __global__ __launch_bounds__(256 * NT) void wgrad_halo_x6_kernel(const WgradPara
     }
 }
 
+// ------------------------------------------ Winograd-domain 3x3 weight gradient (F(2x2, 3x3))
+// The forward of F(2x2,3x3) is y = A^T [ (G g G^T) (.) (B^T d B) ] A (winograd.hip); its
+// derivative w.r.t. the kernel g, summed over the 2x2 output tiles (d = the tile's 4x4 input
+// window, e = its 2x2 output gradient), is
+//     dW = G^T M G,   M_xi[n][c] = sum_tiles Ehat_xi[tile][n] Dhat_xi[tile][c]  (xi = 16 positions)
+// with Ehat = A e A^T and Dhat = B^T d B - both formed with +-1 adds only, so every operand is an
+// fp32 value that splits exactly into hi/mid/lo bf16 and the products are the same 6-term fp32
+// arithmetic as every other weight gradient here, accumulated in fp32.  16 products per tile and
+// (n, c) instead of the direct 36 (9 taps x 4 pixels): 2.25x fewer MFMAs.  G^T M G (factors 1/2,
+// exact scalings) runs once per block on its fp32 partial M, so the slab keeps the direct
+// kernels' [split][n][tap * C + c] layout (+ the bias column) and the same fixed-order fp64
+// reduction finishes it - deterministic.
+//
+// Block: 64 output x 64 input channels x all 16 positions over a contiguous range of tiles (one
+// split), 8 waves; wave (wc, wn, wj) accumulates 32 input x 32 output channels for the 8 positions
+// (i, 2 wj + jj): 128 accumulators.  A stage is 16 tiles = one k-step of v_mfma_f32_32x32x16_bf16,
+// split into 4 sub-stages, one per row i of the positions (as winograd.hip).  Thread (tile pt,
+// channel pair cp) keeps its tile's 4x4 window (2 input channels) and 2x2 gradient tile (2 output
+// channels) in registers and forms row i of Dhat and Ehat for the next sub-stage while the MFMAs
+// of the current one run; the planes go to LDS as [tile row][64 channels] bf16 images (128-byte
+// rows, the halo kernel's swizzle) read back with ds_read_b64_tr_b16 (k = tile).  Each window row
+// is reloaded for the next stage as soon as its last transform is formed (>= 2 sub-stages of
+// cover).  Ehat is formed with the sign-normalised A' = [1 0; 1 1; 1 -1; 0 1] (A's row 3 is
+// [0 -1]): M_xi = s_i s_j M'_xi, s = (1, 1, 1, -1), applied in the output transform.
+constexpr int WW_IMG = 16 * 128;           // one (position, plane) image: 16 tile rows x 64 channels
+constexpr int WW_SLOT = 4 * 3 * WW_IMG;    // one operand, one sub-stage: 4 positions x 3 planes
+
+struct WinoWgradParams {
+    WgradParams p;
+    int tiles, tps;            // tiles (batch x Ho/2 x Wo/2); tiles per split (multiple of 16)
+    FastDiv dTw, dTh;          // tile index -> (image, tile row, tile column)
+    unsigned x0_bytes, x1_bytes, p_bytes;   // buffer ranges (sources shifted back by Wi + 1 pixels)
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ww_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long b = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// x -> hi/mid/lo bf16 of both lanes of the pair, packed (x = hi + mid + lo exactly)
+__device__ __forceinline__ void ww_split(const wg_f32x2 x, unsigned& h, unsigned& m, unsigned& l) {
+#pragma clang fp contract(off)
+    const unsigned a = wg_pk(x);
+    const float r0 = x[0] - __builtin_bit_cast(float, a << 16);
+    const float r1 = x[1] - __builtin_bit_cast(float, a & 0xffff0000u);
+    const unsigned b = wg_pk(wg_f32x2{r0, r1});
+    const float l0 = r0 - __builtin_bit_cast(float, b << 16);
+    const float l1 = r1 - __builtin_bit_cast(float, b & 0xffff0000u);
+    h = a;
+    m = b;
+    l = wg_pk(wg_f32x2{l0, l1});
+}
+
+__global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParams w) {
+#pragma clang fp contract(off)
+    const WgradParams& p = w.p;
+    // two sub-stage slots per operand; after the loop the first 48 KB carry the output-transform
+    // exchange
+    __shared__ __attribute__((aligned(16))) char ww_lds[4 * WW_SLOT];
+    char* const lx0 = ww_lds;
+    char* const lx1 = ww_lds + WW_SLOT;
+    char* const lg0 = ww_lds + 2 * WW_SLOT;
+    char* const lg1 = ww_lds + 3 * WW_SLOT;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wc = wave & 1, wn = (wave >> 1) & 1, wj = wave >> 2;
+    // logical block (split z, output block ny, input block cx), cx fastest: the blocks an XCD runs
+    // together read the same tiles
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int cx = blk % p.gx;
+    const int rest = blk / p.gx;
+    const int ny = rest % p.gy;
+    const int z = rest / p.gy;
+    const int t_begin = z * w.tps;
+    const int t_end = min(w.tiles, t_begin + w.tps);
+    const int S = (t_end - t_begin + 15) >> 4;
+
+    // ---- producer role: tile pt of a stage, channel pair cp of the 64 input / 64 output channels
+    const int pt = tid >> 5, cp = tid & 31;
+    const int c_lo = cx * 64;
+    const bool first = c_lo < p.c0;
+    const int cs = first ? p.c0 : p.c1;       // pixel stride of the input block's source
+    const int shift = p.Wi + 1;               // window corner (2ty-1, 2tx-1) >= (-1, -1)
+    const __amdgpu_buffer_rsrc_t xr = ww_rsrc((first ? p.src0 : p.src1) - (long long)shift * cs,
+                                              first ? w.x0_bytes : w.x1_bytes);
+    const __amdgpu_buffer_rsrc_t gr = ww_rsrc(p.P, w.p_bytes);
+    const unsigned pixb = (unsigned)cs * 4u;
+    const unsigned xco = (unsigned)((first ? c_lo : c_lo - p.c0) + 2 * cp) * 4u;
+    const unsigned gco = (unsigned)(ny * 64 + 2 * cp) * 4u;
+    const unsigned gpix = (unsigned)p.N * 4u;
+    const int st_off = hx_off(pt, 2 * cp);    // the thread's 4-byte slot in every image
+
+    // window rows of a stage as the loader sees them (byte offsets; LEAN_OOB: zeros)
+    unsigned xv[4];
+    bool xc0 = false, xc3 = false;
+    auto decode_x = [&](int k) {
+        const int m = t_begin + 16 * k + pt;
+        const bool mv = m < t_end;
+        int ty = 0, tx = 0, b = 0;
+        if (mv) {
+            const int t2 = fdiv(m, w.dTw);
+            tx = m - t2 * (p.Wo >> 1);
+            b = fdiv(t2, w.dTh);
+            ty = t2 - b * (p.Ho >> 1);
+        }
+        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs) * 4u + xco;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            xv[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi) * pixb : LEAN_OOB;
+        xc0 = x0 >= 0;
+        xc3 = x0 + 3 < p.Wi;
+    };
+    unsigned gv[2];
+    auto decode_g = [&](int k) {
+        const int m = t_begin + 16 * k + pt;
+        if (m < t_end) {
+            const int t2 = fdiv(m, w.dTw);
+            const int tx = m - t2 * (p.Wo >> 1);
+            const int b = fdiv(t2, w.dTh);
+            const int ty = t2 - b * (p.Ho >> 1);
+            const unsigned base = (unsigned)((b * p.Ho + 2 * ty) * p.Wo + 2 * tx) * gpix + gco;
+            gv[0] = base;
+            gv[1] = base + (unsigned)p.Wo * gpix;
+        } else {
+            gv[0] = gv[1] = LEAN_OOB;
+        }
+    };
+    wg_f32x2 d[4][4], e[2][2];
+    auto load_x = [&](int r) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            unsigned vo = xv[r];
+            if (s == 0) vo = xc0 ? vo : LEAN_OOB;
+            if (s == 3) vo = xc3 ? vo : LEAN_OOB;
+            d[r][s] = __builtin_bit_cast(wg_f32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                       xr, vo, __builtin_amdgcn_readfirstlane(s * pixb), 0));
+        }
+    };
+    auto load_g = [&](int a) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            e[a][s] = __builtin_bit_cast(wg_f32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                       gr, gv[a], __builtin_amdgcn_readfirstlane(s * gpix), 0));
+    };
+    // row i of Dhat (B^T d B) and Ehat (A' e A'^T) for this thread's pairs -> bf16 planes in the
+    // sub-stage slots sx / sg: image (j, plane) at (3 j + plane) * WW_IMG
+    auto form = [&](auto i_c, char* sx, char* sg) {
+        constexpr int i = decltype(i_c)::value;
+        wg_f32x2 t[4], u[2];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if constexpr (i == 0) t[s] = d[0][s] - d[2][s];
+            else if constexpr (i == 1) t[s] = d[1][s] + d[2][s];
+            else if constexpr (i == 2) t[s] = d[2][s] - d[1][s];
+            else t[s] = d[1][s] - d[3][s];
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            if constexpr (i == 0) u[s] = e[0][s];
+            else if constexpr (i == 1) u[s] = e[0][s] + e[1][s];
+            else if constexpr (i == 2) u[s] = e[0][s] - e[1][s];
+            else u[s] = e[1][s];
+        }
+        const wg_f32x2 dv[4] = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+        const wg_f32x2 ev[4] = {u[0], u[0] + u[1], u[0] - u[1], u[1]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            unsigned h, m, l;
+            ww_split(dv[j], h, m, l);
+            char* b = sx + 3 * j * WW_IMG + st_off;
+            *reinterpret_cast<unsigned*>(b) = h;
+            *reinterpret_cast<unsigned*>(b + WW_IMG) = m;
+            *reinterpret_cast<unsigned*>(b + 2 * WW_IMG) = l;
+            ww_split(ev[j], h, m, l);
+            b = sg + 3 * j * WW_IMG + st_off;
+            *reinterpret_cast<unsigned*>(b) = h;
+            *reinterpret_cast<unsigned*>(b + WW_IMG) = m;
+            *reinterpret_cast<unsigned*>(b + 2 * WW_IMG) = l;
+        }
+    };
+
+    // ---- MFMA role: transposed fragment reads as in wgrad_halo_x6_kernel (k = tile row)
+    const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
+    const int rsub = 8 * (grp >> 1) + gq;
+    const int ccol = 16 * (grp & 1) + 4 * gp;
+    const int xa = hx_off(rsub, wc * 32 + ccol) + 2 * wj * 3 * WW_IMG;
+    const int ga = hx_off(rsub, wn * 32 + ccol) + 2 * wj * 3 * WW_IMG;
+    auto tr2 = [&](const char* a) {
+        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a);
+        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a + 4 * 128));
+        typedef short wi16x8 __attribute__((ext_vector_type(8)));
+        const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        return __builtin_bit_cast(wg_bf16x8, av);
+    };
+    f32x16 acc[8];                            // [i][jj]: position (i, 2 wj + jj)
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+    auto mma = [&](auto x_c, const char* sx, const char* sg, int jj) {
+        constexpr int x = decltype(x_c)::value;
+        const char* xb = sx + xa + jj * 3 * WW_IMG;
+        const char* gb = sg + ga + jj * 3 * WW_IMG;
+        const wg_bf16x8 qh = tr2(xb), qm = tr2(xb + WW_IMG), ql = tr2(xb + 2 * WW_IMG);
+        const wg_bf16x8 ph = tr2(gb), pm = tr2(gb + WW_IMG), pl = tr2(gb + 2 * WW_IMG);
+        f32x16 c = acc[x];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm, c, 0, 0, 0);   // small terms first
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, ph, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, pm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh, ph, c, 0, 0, 0);
+        acc[x] = c;
+    };
+    wg_f32x2 bsum = {0.f, 0.f};               // dbias partial of the thread's output pair
+
+    // sub-stage (k, i): MFMAs of row i from slot i & 1, row i + 1 (or the next stage's row 0)
+    // formed into the other slot, then the window / gradient rows whose last use that was are
+    // reloaded for the next stage (x row 0 two stages ahead: its stage-k + 1 copy was formed in
+    // the sub-stage before)
+    auto sub = [&](int k, auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        char* sx = (i & 1) ? lx1 : lx0;
+        char* sg = (i & 1) ? lg1 : lg0;
+        char* nx = (i & 1) ? lx0 : lx1;
+        char* ng = (i & 1) ? lg0 : lg1;
+        mma(std::integral_constant<int, 2 * i>{}, sx, sg, 0);
+        if constexpr (i < 3) {
+            form(std::integral_constant<int, i + 1>{}, nx, ng);
+        } else {
+            if (k + 1 < S) form(std::integral_constant<int, 0>{}, nx, ng);
+        }
+        if constexpr (i == 1) {               // d row 2 and e row 0 are dead: next stage's
+            load_x(2);
+            bsum += e[0][0] + e[0][1];
+            decode_g(k + 1);
+            load_g(0);
+        } else if constexpr (i == 2) {        // d rows 1, 3 and e row 1 are dead
+            load_x(1);
+            load_x(3);
+            bsum += e[1][0] + e[1][1];
+            load_g(1);
+        } else if constexpr (i == 3) {        // d row 0 of stage k + 1 was used: stage k + 2's
+            decode_x(k + 2);
+            load_x(0);
+        }
+        mma(std::integral_constant<int, 2 * i + 1>{}, sx, sg, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");     // s_barrier is no compiler fence: keep LDS reads behind it
+    };
+
+    // prologue: stage 0 whole, sub-stage (0, 0) formed, stage 1's row 0 in flight
+    decode_x(0);
+    load_x(0);
+    load_x(1);
+    load_x(2);
+    load_x(3);
+    decode_g(0);
+    load_g(0);
+    load_g(1);
+    if (S > 0) form(std::integral_constant<int, 0>{}, lx0, lg0);
+    decode_x(1);
+    load_x(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int k = 0; k < S; ++k) {
+        sub(k, std::integral_constant<int, 0>{});
+        sub(k, std::integral_constant<int, 1>{});
+        sub(k, std::integral_constant<int, 2>{});
+        sub(k, std::integral_constant<int, 3>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // trailing (empty-range) loads
+
+    float* slab = p.slab + (long long)z * p.Nr * p.Kcp;
+    // ---- bias: column sums of dZ over the split, fixed order (thread stages, then the 16 tiles)
+    if (p.bias_mode == 1 && cx == 0) {
+        wg_f32x2* red = reinterpret_cast<wg_f32x2*>(lg0);
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < 32) {
+            wg_f32x2 v = red[tid];
+            for (int r = 1; r < 16; ++r) v += red[r * 32 + tid];
+            slab[(long long)(ny * 64 + 2 * tid) * p.Kcp + p.K] = v[0];
+            slab[(long long)(ny * 64 + 2 * tid + 1) * p.Kcp + p.K] = v[1];
+        }
+        __syncthreads();
+    }
+
+    // ---- output transform dW = G^T M G (G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]).  Over the rows
+    // first (the wave holds all 4 rows of its 2 columns j): R[r][j] = sum_a G[a][r] M[a][j]; then
+    // dW[r][s] = sum_j R[r][j] G[j][s] = P0[r][s] + P1[r][s], P0 from j = 0, 1 (wj = 0), P1 from
+    // j = 2, 3 (wj = 1).  The two waves of a (wc, wn) pair swap halves through LDS: wave wj
+    // finishes the channel groups q = 2 wj, 2 wj + 1 of its accumulators.  Signs: M = s_i s_j M'.
+    const float sj1 = wj ? -1.f : 1.f;        // s_j of column jj = 1 (j = 3 for wj = 1)
+    float* xs = reinterpret_cast<float*>(lx0) + ((wc * 2 + wn) * 2 + wj) * 24 * 64;   // 4 pairs x 2 x 6 KB
+    const float* xrd = reinterpret_cast<const float*>(lx0) + ((wc * 2 + wn) * 2 + (1 - wj)) * 24 * 64;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int n = ny * 64 + wn * 32 + lr;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        float mine[2][3][4], other[2][3][4];  // [q half][s][e]
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int ee = 0; ee < 4; ++ee) {
+                const int idx = 4 * q + ee;
+                float R[2];
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    // M[a][j] = s_a s_j M'[a][j]: s_3 = -1 on row a = 3 and on column j = 3
+                    const float m0 = acc[0 * 2 + jj][idx], m1 = acc[1 * 2 + jj][idx];
+                    const float m2 = acc[2 * 2 + jj][idx], m3 = -acc[3 * 2 + jj][idx];
+                    float v = r == 0 ? m0 + 0.5f * (m1 + m2) : r == 1 ? 0.5f * (m1 - m2) : 0.5f * (m1 + m2) + m3;
+                    R[jj] = jj == 1 ? sj1 * v : v;
+                }
+                // this wave's share of dW[r][s] for s = 0..2
+                float P[3];
+                if (wj == 0) {            // j = 0, 1: R0 G[0] + R1 G[1]
+                    P[0] = R[0] + 0.5f * R[1];
+                    P[1] = 0.5f * R[1];
+                    P[2] = 0.5f * R[1];
+                } else {                  // j = 2, 3: R2 G[2] + R3 G[3]
+                    P[0] = 0.5f * R[0];
+                    P[1] = -0.5f * R[0];
+                    P[2] = 0.5f * R[0] + R[1];
+                }
+                const bool keep = (q >> 1) == wj;
+#pragma unroll
+                for (int s = 0; s < 3; ++s) {
+                    if (keep) mine[q & 1][s][ee] = P[s];
+                    else other[q & 1][s][ee] = P[s];
+                }
+            }
+        // send the partner's half: [qh][s][e] -> 24 floats per lane
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+#pragma unroll
+                for (int ee = 0; ee < 4; ++ee) xs[((qh * 3 + s) * 4 + ee) * 64 + lane] = other[qh][s][ee];
+        __syncthreads();
+#pragma unroll
+        for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                f32x4 v;
+#pragma unroll
+                for (int ee = 0; ee < 4; ++ee) {
+                    const float o = xrd[((qh * 3 + s) * 4 + ee) * 64 + lane];
+                    // P0 + P1 in that order on both waves of the pair
+                    v[ee] = wj == 0 ? mine[qh][s][ee] + o : o + mine[qh][s][ee];
+                }
+                const int q = 2 * wj + qh;
+                const int k = (3 * r + s) * p.C + c_lo + wc * 32 + 8 * q + 4 * lh;
+                *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
+            }
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------- single-channel stem weight gradient
 // dW[n][tap] = sum_m dZ[m][n] x[m + tap] and db[n] = sum_m dZ[m][n] for the 1 -> N stem conv
 // (inc.c0): the layer is the read of dZ (N channels per pixel).  Blocks sweep 16 x 64 pixel tiles
@@ -1175,6 +1543,8 @@ __global__ __launch_bounds__(576) void wgrad_finish_t_kernel(const T* __restrict
 struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
     bool qvec, dma, small, halo, stem;
+    bool wino = false;                        // Winograd-domain kernel (wgrad_wino_x6_kernel)
+    int tiles = 0, tps = 0;
     int nt = 1;                               // halo kernel: 64-channel output tiles per block
     int tiles_w, tiles_h;
     size_t slab_bytes() const { return (size_t)splits * Nr * Kcp * sizeof(float); }
@@ -1194,6 +1564,26 @@ static bool small_wgrad_ok(const pu_wgrad_args* a) {
            (a->n == 4 || a->n == 8 || a->n == 16) && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
            a->in_h == a->out_h && a->in_w == a->out_w && a->bias_mode != 2 &&
            (C == 1 || (a->c0 % 4 == 0 && a->c1 % 4 == 0));
+}
+
+static void plan_groups(WgradPlan* pl);
+
+// the Winograd-domain kernel: 3x3 / s1 / p1 on an even same-size grid, 64-channel input blocks
+// from one source each, 64-channel output blocks, the 6-product arithmetic, byte offsets of the
+// (shifted) sources and of dZ under 2^31; PU_WINO_WGRAD=0 keeps the direct kernels (A/B runs)
+static bool wino_wgrad_ok(const pu_wgrad_args* a, const WgradPlan* pl) {
+    static const bool on = [] {
+        const char* e = getenv("PU_WINO_WGRAD");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || a->math != 1 || !pl->qvec) return false;
+    if (a->kh != 3 || a->kw != 3 || a->stride != 1 || a->pad != 1) return false;
+    if (a->in_h != a->out_h || a->in_w != a->out_w || (a->out_h & 1) || (a->out_w & 1)) return false;
+    if (a->c0 % 64 || a->c1 % 64 || a->n % 64 || a->bias_mode == 2) return false;
+    const long long px = (long long)a->batch * a->in_h * a->in_w + a->in_w + 1;
+    if (px * (a->c0 > a->c1 ? a->c0 : a->c1) * 4 >= (1LL << 31)) return false;
+    if ((long long)a->batch * a->out_h * a->out_w * a->n * 4 >= (1LL << 31)) return false;
+    return (((uintptr_t)a->rows | (uintptr_t)a->src0 | (uintptr_t)a->src1) & 7) == 0;
 }
 
 // Measured alternatives: capping the GEMM-path split count at 2 / 4 (round 3: C2 4060 -> 2262 /
@@ -1261,6 +1651,25 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
         occ = 2;
     }
     pl->halo = false;
+    if (wino_wgrad_ok(a, pl)) {
+        // one 512-thread block per CU: (C / 64) x (N / 64) channel blocks x tile splits of whole
+        // 16-tile stages
+        pl->wino = true;
+        pl->BN = 64;
+        pl->BK = 9 * 64;
+        pl->gx = pl->C / 64;
+        pl->gy = a->n / 64;
+        pl->tiles = a->batch * (a->out_h / 2) * (a->out_w / 2);
+        const int stages = ceil_div(pl->tiles, 16);
+        int splits = 256 / (pl->gx * pl->gy);
+        if (splits > stages) splits = stages;
+        if (splits < 1) splits = 1;
+        pl->tps = ceil_div(stages, splits) * 16;
+        pl->splits = ceil_div(pl->tiles, pl->tps);
+        pl->mps = pl->tps * 4;
+        plan_groups(pl);
+        return PU_OK;
+    }
     if (a->math == 1 && pl->dma && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
         a->in_h == a->out_h && a->in_w == a->out_w && a->out_w % 16 == 0 && a->c0 % 64 == 0 && a->c1 % 64 == 0 &&
         a->n % 64 == 0 && a->bias_mode != 2 && (long long)a->batch * a->in_h * a->in_w * (pl->C) < (1LL << 31)) {
@@ -1874,7 +2283,7 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
     if (st != PU_OK) return st;
     if (bn) *bn = pl.BN;
     if (bk) *bk = pl.BK;
-    if (qvec) *qvec = pl.stem ? 4 : pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo, 4: stem
+    if (qvec) *qvec = pl.wino ? 5 : pl.stem ? 4 : pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo, 4: stem, 5: Winograd
     if (splits) *splits = pl.splits;
     return PU_OK;
 }
@@ -1934,7 +2343,19 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
         else hipLaunchKernelGGL((wgrad_dma_kernel<BN_, BK_, WN_, WK_, 3, false>), grid, dim3(256), 0, s, p); \
     } while (0)
 #define PU_WG_REG(BN_, BK_, WN_, WK_, Q_) hipLaunchKernelGGL((wgrad_kernel<BN_, BK_, WN_, WK_, Q_>), grid, dim3(256), 0, s, p)
-        if (pl.halo) {
+        if (pl.wino) {
+            WinoWgradParams ww;
+            ww.p = p;
+            ww.tiles = pl.tiles;
+            ww.tps = pl.tps;
+            ww.dTw = make_fastdiv(a->out_w / 2);
+            ww.dTh = make_fastdiv(a->out_h / 2);
+            const long long px = (long long)a->batch * a->in_h * a->in_w + a->in_w + 1;
+            ww.x0_bytes = (unsigned)(px * a->c0 * 4);
+            ww.x1_bytes = (unsigned)(px * a->c1 * 4);
+            ww.p_bytes = (unsigned)((long long)pl.M * a->n * 4);
+            hipLaunchKernelGGL(wgrad_wino_x6_kernel, grid, dim3(512), 0, s, ww);
+        } else if (pl.halo) {
             if (pl.nt == 2) hipLaunchKernelGGL(wgrad_halo_x6_kernel<2>, grid, dim3(512), 0, s, p);
             else hipLaunchKernelGGL(wgrad_halo_x6_kernel<1>, grid, dim3(256), 0, s, p);
         } else if (pl.dma) {

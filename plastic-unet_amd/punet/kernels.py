@@ -321,14 +321,25 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct", "halo", "stem")[qv.value])
-    if a.math == 1 and qv.value in (1, 3):
+    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct", "halo", "stem", "wino")[qv.value])
+    if a.math == 1 and qv.value in (1, 3, 5):
         tag = tag[:-1] + ",x6>"
     # the GEMM and the split reduction timed apart (they are separate kernels in rocprof too)
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
         check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 1, _stream()), "pu_wgrad_phase")
     with _Rec("wgrad_reduce", nbytes=float(nbytes)):
         check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 2, _stream()), "pu_wgrad_phase")
+
+
+def wgrad_kind(*, batch, hw, n, c0, c1=0):
+    """Which kernel pu_wgrad takes for an fp32 3x3/s1/p1 same-size weight gradient (pu_wgrad_tile's
+    loader kind: 1 float4 GEMM, 2 small-channel direct, 3 halo, 4 stem, 5 Winograd-domain)."""
+    a = WgradArgs(batch, hw[0], hw[1], hw[0], hw[1], 3, 3, 1, 1, 16, n, 16, c0, 16 if c1 else None, c1, 1, 16, 16,
+                  0, 1 if _FP32_MATH == "split6" else 0)
+    bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib().pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp)),
+          "pu_wgrad_tile")
+    return qv.value
 
 
 def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):

@@ -160,3 +160,16 @@ def test_wino_plan_reported_and_split_k():
     direct = args(32, 128, 64, 64, False)
     L.pu_conv_igemm_tile(ctypes.byref(direct), *(ctypes.byref(v) for v in (bm, bn, mode, ks)))
     assert mode.value == 4
+
+
+def test_wgrad_dispatch_plan_takes_winograd_on_c2_layers():
+    """Planning only (no GPU): the C2 3x3 weight gradients (64-channel blocks, even grids) take the
+    Winograd-domain kernel (kind 5), the 8/16-channel and odd-grid ones do not; the workspace is
+    the slab of one 512-thread block per CU."""
+    from punet import kernels as K
+    for (B, H, c0, c1, n) in [(32, 128, 64, 0, 64), (32, 128, 64, 64, 64), (32, 64, 128, 0, 128),
+                              (32, 32, 256, 256, 128), (32, 16, 512, 0, 512), (32, 8, 512, 0, 512)]:
+        assert K.wgrad_kind(batch=B, hw=(H, H), n=n, c0=c0, c1=c1) == 5, (H, c0, c1, n)
+    assert K.wgrad_kind(batch=4, hw=(101, 101), n=64, c0=64) != 5       # odd grid
+    assert K.wgrad_kind(batch=4, hw=(64, 64), n=32, c0=32) != 5         # 32-channel layer
+    assert K.wgrad_kind(batch=4, hw=(64, 64), n=8, c0=8) == 2            # small-channel direct

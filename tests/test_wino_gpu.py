@@ -177,3 +177,40 @@ def test_wino_persistent_equals_one_item_per_block(tmp_path):
         out[persist] = torch.load(f, weights_only=True)
     assert torch.equal(out["1"]["y"], out["0"]["y"])
     assert torch.equal(out["1"]["d"], out["0"]["d"])
+
+
+WGRAD_CASES = [
+    # B, H, W, c0, c1, cout
+    (2, 16, 16, 64, 0, 64),       # one channel block; 8x8 tile grid (a 16-tile stage spans 2 tile rows)
+    (3, 10, 14, 128, 0, 128),     # 105 tiles: a ragged last stage, 2 x 2 channel blocks, non-square
+    (2, 8, 8, 64, 64, 64),        # concat (two sources), every tile on an image edge
+    (1, 32, 16, 128, 0, 192),     # 3 output blocks
+    (4, 8, 8, 512, 0, 512),       # 64 channel blocks x 4 splits (the bottom level)
+    (2, 16, 16, 256, 256, 256),   # two 256-channel sources, 8 x 4 blocks
+    (8, 64, 64, 64, 0, 64),       # 256 splits of 32 tiles (the top level's shape at bs 8)
+    (1, 2, 2, 64, 0, 64),         # a single tile
+]
+
+
+@pytest.mark.parametrize("B,H,W,c0,c1,cout", WGRAD_CASES)
+def test_wino_wgrad_vs_fp64(B, H, W, c0, c1, cout):
+    """wgrad_wino_x6_kernel (dW = G^T [sum_tiles (A e A^T)(.)(B^T d B)] G, bias as dZ column sums)
+    against fp64, next to ATen's CPU fp32 error; bitwise run-to-run determinism; and the kernel
+    really is the one dispatched (pu_wgrad_tile kind 5)."""
+    g = torch.Generator().manual_seed(B * 17 + H * 5 + W + c0 + 7 * c1 + cout)
+    C = c0 + c1
+    x = torch.randn(B, C, H, W, generator=g).relu()
+    dz = torch.randn(B, cout, H, W, generator=g) * (torch.rand(B, cout, H, W, generator=g) > 0.3).float()
+    ref = {}
+    for dt in (torch.float32, torch.float64):
+        ref[dt] = (torch.nn.grad.conv2d_weight(x.to(dt), (cout, C, 3, 3), dz.to(dt), padding=1),
+                   dz.to(dt).sum((0, 2, 3)))
+    xk = nhwc(x).to(DEV)
+    x0, x1 = (xk[..., :c0].contiguous(), xk[..., c0:].contiguous()) if c1 else (xk, None)
+    dzk = nhwc(dz).to(DEV)
+    assert K.wgrad_kind(batch=B, hw=(H, W), n=cout, c0=c0, c1=c1) == 5
+    dw, db = T.conv3x3_wgrad(dzk, x0, x1)
+    check("wino wgrad %dx%dx%d %d+%d->%d" % (B, H, W, c0, c1, cout), dw, ref[torch.float32][0], ref[torch.float64][0])
+    check("wino bias grad", db, ref[torch.float32][1], ref[torch.float64][1])
+    dw2, db2 = T.conv3x3_wgrad(dzk, x0, x1)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2), "Winograd weight gradient is not deterministic"
