@@ -51,6 +51,11 @@ def main():
             print("   effective clock GHz          %.3f" % (g / 8.0 / (sum(ds) / len(ds))))
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in c:
             print("   MFMA busy                    %.3f" % (c["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8.0 * 1024)))
+        if g and "SQ_LDS_IDX_ACTIVE" in c:
+            # per CU and GPU cycle (x4 if the counter runs in quad-cycles like SQ_WAVE_CYCLES)
+            print("   LDS active / CU-cycle        %.3f" % (c["SQ_LDS_IDX_ACTIVE"] / (g / 8.0 * 256)))
+        if g and "TA_TA_BUSY_sum" in c:
+            print("   TA busy / CU-cycle           %.3f" % (c["TA_TA_BUSY_sum"] / (g / 8.0 * 256)))
         wc = c.get("SQ_WAVE_CYCLES")
         if wc:
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS",
