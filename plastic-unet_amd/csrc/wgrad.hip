@@ -14,6 +14,15 @@
 #include "common.h"
 #include <type_traits>
 
+#ifndef PU_NO_ILV
+#define PU_NO_ILV 0   // 1: leave MFMA / VALU placement to the scheduler (A/B builds)
+#endif
+// wgrad_wino_x6_kernel ablations (timing only, wrong results): 1 no MFMAs, 2 no plane formation
+// (VALU + LDS stores), 3 no global loads, 4 no per-sub-stage barrier
+#ifndef PU_WW_ABL
+#define PU_WW_ABL 0
+#endif
+
 namespace pu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -813,13 +822,13 @@ __device__ __forceinline__ void ww_split(const wg_f32x2 x, unsigned& h, unsigned
 __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParams w) {
 #pragma clang fp contract(off)
     const WgradParams& p = w.p;
-    // two sub-stage slots per operand; after the loop the first 48 KB carry the output-transform
-    // exchange
-    __shared__ __attribute__((aligned(16))) char ww_lds[4 * WW_SLOT];
-    char* const lx0 = ww_lds;
-    char* const lx1 = ww_lds + WW_SLOT;
-    char* const lg0 = ww_lds + 2 * WW_SLOT;
-    char* const lg1 = ww_lds + 3 * WW_SLOT;
+    // two sub-stage slots per operand, as separate arrays: the compiler then knows that the
+    // plane stores of the next sub-stage (other slot) do not alias this sub-stage's operand reads
+    // and can interleave them; after the loop lx0 / lx1 carry the output-transform exchange
+    __shared__ __attribute__((aligned(16))) char lx0[WW_SLOT];
+    __shared__ __attribute__((aligned(16))) char lx1[WW_SLOT];
+    __shared__ __attribute__((aligned(16))) char lg0[WW_SLOT];
+    __shared__ __attribute__((aligned(16))) char lg1[WW_SLOT];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -889,6 +898,11 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
     };
     wg_f32x2 d[4][4], e[2][2];
     auto load_x = [&](int r) {
+        if (PU_WW_ABL == 3) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) d[r][s] = wg_f32x2{1.f + r, 2.f - s};
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             unsigned vo = xv[r];
@@ -899,6 +913,10 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
         }
     };
     auto load_g = [&](int a) {
+        if (PU_WW_ABL == 3) {
+            e[a][0] = e[a][1] = wg_f32x2{0.5f, 0.25f * a};
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < 2; ++s)
             e[a][s] = __builtin_bit_cast(wg_f32x2, __builtin_amdgcn_raw_buffer_load_b64(
@@ -908,6 +926,7 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
     // sub-stage slots sx / sg: image (j, plane) at (3 j + plane) * WW_IMG
     auto form = [&](auto i_c, char* sx, char* sg) {
         constexpr int i = decltype(i_c)::value;
+        if (PU_WW_ABL == 2) return;
         wg_f32x2 t[4], u[2];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -965,6 +984,12 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
         const char* gb = sg + ga + jj * 3 * WW_IMG;
         const wg_bf16x8 qh = tr2(xb), qm = tr2(xb + WW_IMG), ql = tr2(xb + 2 * WW_IMG);
         const wg_bf16x8 ph = tr2(gb), pm = tr2(gb + WW_IMG), pl = tr2(gb + 2 * WW_IMG);
+        if (PU_WW_ABL == 1) {             // keep the operand reads alive, drop the MFMAs
+            acc[x][0] += __builtin_bit_cast(float, __builtin_shufflevector(qh, qm, 0, 1)) +
+                         __builtin_bit_cast(float, __builtin_shufflevector(ql, ph, 0, 1)) +
+                         __builtin_bit_cast(float, __builtin_shufflevector(pm, pl, 0, 1));
+            return;
+        }
         f32x16 c = acc[x];
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm, pm, c, 0, 0, 0);   // small terms first
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql, ph, c, 0, 0, 0);
@@ -987,11 +1012,9 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
         char* nx = (i & 1) ? lx0 : lx1;
         char* ng = (i & 1) ? lg0 : lg1;
         mma(std::integral_constant<int, 2 * i>{}, sx, sg, 0);
-        if constexpr (i < 3) {
-            form(std::integral_constant<int, i + 1>{}, nx, ng);
-        } else {
-            if (k + 1 < S) form(std::integral_constant<int, 0>{}, nx, ng);
-        }
+        // (past the last stage this forms zeros into a slot no MFMA reads: the sub-stage stays
+        // one basic block for the interleave below)
+        form(std::integral_constant<int, (i + 1) & 3>{}, nx, ng);
         if constexpr (i == 1) {               // d row 2 and e row 0 are dead: next stage's
             load_x(2);
             bsum += e[0][0] + e[0][1];
@@ -1007,9 +1030,24 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
             load_x(0);
         }
         mma(std::integral_constant<int, 2 * i + 1>{}, sx, sg, 1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");     // s_barrier is no compiler fence: keep LDS reads behind it
+        // Interleave: the wave's 12 MFMAs spread over the forming work (~110 VALU + 24 LDS
+        // stores) instead of 6 before and 6 after it - the two waves of a SIMD run the same phase
+        // between barriers, so MFMAs bunched at the ends leave the matrix pipe idle during the VALU
+#if !PU_NO_ILV && PU_WW_ABL == 0
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);       // position 0 operands
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);     // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 9, 0);     // ~1/12 of the VALU
+            __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);     // ~1/12 of the plane stores
+            if (q == 2) __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);   // position 1 operands
+        }
+#endif
+        if (PU_WW_ABL != 4) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");     // s_barrier is no compiler fence: keep LDS reads behind it
+        }
     };
 
     // prologue: stage 0 whole, sub-stage (0, 0) formed, stage 1's row 0 in flight
@@ -1021,7 +1059,7 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
     decode_g(0);
     load_g(0);
     load_g(1);
-    if (S > 0) form(std::integral_constant<int, 0>{}, lx0, lg0);
+    form(std::integral_constant<int, 0>{}, lx0, lg0);
     decode_x(1);
     load_x(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1056,8 +1094,9 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
     // j = 2, 3 (wj = 1).  The two waves of a (wc, wn) pair swap halves through LDS: wave wj
     // finishes the channel groups q = 2 wj, 2 wj + 1 of its accumulators.  Signs: M = s_i s_j M'.
     const float sj1 = wj ? -1.f : 1.f;        // s_j of column jj = 1 (j = 3 for wj = 1)
-    float* xs = reinterpret_cast<float*>(lx0) + ((wc * 2 + wn) * 2 + wj) * 24 * 64;   // 4 pairs x 2 x 6 KB
-    const float* xrd = reinterpret_cast<const float*>(lx0) + ((wc * 2 + wn) * 2 + (1 - wj)) * 24 * 64;
+    // 6 KB per wave: the wc = 0 pairs in lx0, the wc = 1 pairs in lx1
+    float* xs = reinterpret_cast<float*>(wc ? lx1 : lx0) + (wn * 2 + wj) * 24 * 64;
+    const float* xrd = reinterpret_cast<const float*>(wc ? lx1 : lx0) + (wn * 2 + (1 - wj)) * 24 * 64;
     const int lr = lane & 31, lh = lane >> 5;
     const int n = ny * 64 + wn * 32 + lr;
 #pragma unroll
@@ -2172,7 +2211,10 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
     const dim3 fgrid((unsigned)((threads + 255) / 256));
     const int taps = a->kh * a->kw;
-    if ((pl.small || pl.stem) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
+    // one launch for many splits of a few-thousand-entry slab (the direct small-channel / stem
+    // kernels, and the Winograd-domain kernel's 64 x 64 blocks at the 128^2 / 64^2 levels: 64-256
+    // splits), instead of the two-pass grouped form
+    if ((pl.small || pl.stem || (pl.wino && pl.splits >= 32)) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
         hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)ceil_div(total, (long long)WR_E)), dim3(256), 0, s,
                            (const float*)workspace, pl.splits, total, a->n, pl.Kcp, pl.K, pl.C, a->kh, a->kw,
                            a->bias_mode, a->dweight, a->dbias, a->accumulate);

@@ -35,6 +35,15 @@
 //     igemm_splitk_epilogue_kernel.
 #include "conv_common.h"
 
+#ifndef PU_NO_ILV
+#define PU_NO_ILV 0   // 1: leave MFMA / VALU placement to the scheduler (A/B builds)
+#endif
+// wino_x6_kernel ablations (timing only, wrong results): 1 no MFMAs, 2 no V formation (VALU + LDS
+// stores), 3 no window loads, 4 no per-sub-stage barrier (the waits stay), 5 no U DMA
+#ifndef PU_WF_ABL
+#define PU_WF_ABL 0
+#endif
+
 namespace pu {
 
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -182,6 +191,11 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 
     // window row rr (4 pixels x 2 channels) of chunk kc of item I (zeros past its chunks)
     auto load_row = [&](const Item& I, int kc, int rr) {
+        if (PU_WF_ABL == 3) {
+#pragma unroll
+            for (int ss = 0; ss < 4; ++ss) d[rr * 4 + ss] = f32x2v{1.f + rr, 0.5f * ss};
+            return;
+        }
         const int c = kc * 16;
         const bool second = c >= p.c0;
         const bool ok = I.live && kc < I.kc1;
@@ -198,6 +212,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     };
     // U pieces of sub-stage (chunk kc, row i) of item I into U slot base (zeros past its chunks)
     auto load_u = [&](const Item& I, int kc, int i, unsigned char* base) {
+        if (PU_WF_ABL == 5) return;
         const unsigned bytes = I.live && kc < I.kc1 ? w.u_bytes : 0u;
         const unsigned sb = (unsigned)((kc * 16 + 4 * i) * 3) * u_row + (unsigned)(I.n_blk * 32);
 #pragma unroll
@@ -206,6 +221,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     // V = row i of B^T d B for this thread's 2 channels -> hi/mid/lo planes in V slot sb
     auto make_v = [&](auto i_c, unsigned char* sb) {
         constexpr int i = decltype(i_c)::value;
+        if (PU_WF_ABL == 2) return;
         f32x2v t[4];
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
@@ -235,6 +251,12 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
             fu[pl] = *reinterpret_cast<const bf16x8_t*>(ub + pl * 2048);
             fv[pl] = *reinterpret_cast<const bf16x8_t*>(vb + pl * 2048);
         }
+        if (PU_WF_ABL == 1) {
+            acc[x][0] += __builtin_bit_cast(float, __builtin_shufflevector(fu[0], fu[1], 0, 1)) +
+                         __builtin_bit_cast(float, __builtin_shufflevector(fu[2], fv[0], 0, 1)) +
+                         __builtin_bit_cast(float, __builtin_shufflevector(fv[1], fv[2], 0, 1));
+            return;
+        }
         f32x16 c = acc[x];
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[1], fv[1], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[2], fv[0], c, 0, 0, 0);
@@ -261,7 +283,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         else if constexpr (i == 1) asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
         else if constexpr (i == 2) asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(22) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if (PU_WF_ABL != 4) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if constexpr (i == 0) load_u(cur, kc, 3, fu);
         else load_u(T, tkc, i - 1, fu);
@@ -276,6 +298,19 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
             load_row(T, tkc, 3);
         }
         mma(std::integral_constant<int, 2 * i + 1>{}, cv, cu, 1);
+#if !PU_NO_ILV && PU_WF_ABL == 0
+        // Interleave the 12 MFMAs with the V formation (~55 VALU, 12 plane stores): left to
+        // itself the scheduler bunches 6 MFMAs before and 6 after it, and the two waves of a SIMD,
+        // in the same phase between barriers, leave the matrix pipe idle during the VALU
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);        // position 2i operands
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            if (q == 2) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);   // position 2i + 1 operands
+        }
+#endif
     };
 
     // stream prologue: the first item's whole first window, U of sub-stages 0..2, V of 0
@@ -442,53 +477,54 @@ __global__ __launch_bounds__(256) void wino_pack_kernel(const WinoPackBatch bt) 
     int j = 0, b0 = 0;
     while (j + 1 < bt.count && (int)blockIdx.x >= b0 + bt.job[j].blocks) b0 += bt.job[j++].blocks;
     const WinoPackJob J = bt.job[j];
-    // lane = (chunk, n, half): neighbouring lanes write neighbouring 16-byte halves of one
-    // 32-byte U row, so every store instruction covers a contiguous 1 KB
+    // thread = (row a of G g G^T, chunk, n, half), a slowest: neighbouring lanes write
+    // neighbouring 16-byte halves of one 32-byte U row, so every store instruction covers a
+    // contiguous 1 KB; one row per thread keeps ~100 VGPRs (4 rows per thread: 244, 2 waves per
+    // SIMD - too few loads in flight, 2.3 TB/s)
     const int idx = ((int)blockIdx.x - b0) * 256 + threadIdx.x;
     const int c8s = J.c / 8;
-    if (idx >= J.n * c8s) return;
-    const int nh = idx >> 1;
+    const int per_a = J.n * c8s;
+    if (idx >= 4 * per_a) return;
+    const int a = idx / per_a;
+    const int rest = idx - a * per_a;
+    const int nh = rest >> 1;
     const int n = nh % J.n;
-    const int c8 = (nh / J.n) * 2 + (idx & 1);
+    const int c8 = (nh / J.n) * 2 + (rest & 1);
     typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
     const int chunk = c8 >> 1, half = c8 & 1;
-    // one row a of G g G^T at a time (12 output vectors live instead of 48)
-#pragma unroll 1
-    for (int a = 0; a < 4; ++a) {
-        bf16x8v o[4][3];
+    bf16x8v o[4][3];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int c = c8 * 8 + e;
-            double g[3][3];
+    for (int e = 0; e < 8; ++e) {
+        const int c = c8 * 8 + e;
+        double g[3][3];
 #pragma unroll
-            for (int r = 0; r < 3; ++r)
-#pragma unroll
-                for (int s = 0; s < 3; ++s)
-                    g[r][s] = J.dgrad ? (double)J.w[(((long long)c * J.n + n) * 3 + (2 - r)) * 3 + (2 - s)]
-                                      : (double)J.w[(((long long)n * J.c + c) * 3 + r) * 3 + s];
-            double t[3];   // row a of G g
+        for (int r = 0; r < 3; ++r)
 #pragma unroll
             for (int s = 0; s < 3; ++s)
-                t[s] = a == 0 ? g[0][s] : a == 1 ? 0.5 * (g[0][s] + g[1][s] + g[2][s])
-                     : a == 2 ? 0.5 * (g[0][s] - g[1][s] + g[2][s]) : g[2][s];
-            const double u[4] = {t[0], 0.5 * (t[0] + t[1] + t[2]), 0.5 * (t[0] - t[1] + t[2]), t[2]};
+                g[r][s] = J.dgrad ? (double)J.w[(((long long)c * J.n + n) * 3 + (2 - r)) * 3 + (2 - s)]
+                                  : (double)J.w[(((long long)n * J.c + c) * 3 + r) * 3 + s];
+        double t[3];   // row a of G g
 #pragma unroll
-            for (int bc = 0; bc < 4; ++bc) {
-                const float x = (float)u[bc];
-                const __bf16 h = (__bf16)x;
-                const float rr = x - (float)h;
-                const __bf16 mm = (__bf16)rr;
-                o[bc][0][e] = h;
-                o[bc][1][e] = mm;
-                o[bc][2][e] = (__bf16)(rr - (float)mm);
-            }
+        for (int s = 0; s < 3; ++s)
+            t[s] = a == 0 ? g[0][s] : a == 1 ? 0.5 * (g[0][s] + g[1][s] + g[2][s])
+                 : a == 2 ? 0.5 * (g[0][s] - g[1][s] + g[2][s]) : g[2][s];
+        const double u[4] = {t[0], 0.5 * (t[0] + t[1] + t[2]), 0.5 * (t[0] - t[1] + t[2]), t[2]};
+#pragma unroll
+        for (int bc = 0; bc < 4; ++bc) {
+            const float x = (float)u[bc];
+            const __bf16 h = (__bf16)x;
+            const float rr = x - (float)h;
+            const __bf16 mm = (__bf16)rr;
+            o[bc][0][e] = h;
+            o[bc][1][e] = mm;
+            o[bc][2][e] = (__bf16)(rr - (float)mm);
         }
-#pragma unroll
-        for (int bc = 0; bc < 4; ++bc)
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-                *reinterpret_cast<bf16x8v*>(J.out + ((((long long)chunk * 16 + a * 4 + bc) * 3 + pl) * J.n + n) * 16 + half * 8) = o[bc][pl];
     }
+#pragma unroll
+    for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+            *reinterpret_cast<bf16x8v*>(J.out + ((((long long)chunk * 16 + a * 4 + bc) * 3 + pl) * J.n + n) * 16 + half * 8) = o[bc][pl];
 }
 
 // host side -------------------------------------------------------------------------------------
@@ -602,7 +638,7 @@ extern "C" int pu_pack_wino(const pu_wino_job* jobs, int n_jobs, void* stream) {
             o.n = n;
             o.c = c;
             o.dgrad = J.dgrad != 0;
-            o.blocks = ceil_div((long long)n * (c / 8), 256);
+            o.blocks = ceil_div(4LL * n * (c / 8), 256);   // one thread per (row a, n, 8 channels)
             total += o.blocks;
         }
         hipLaunchKernelGGL(wino_pack_kernel, dim3((unsigned)total), dim3(256), 0, as_stream(stream), b);
