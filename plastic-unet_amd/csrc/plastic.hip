@@ -385,6 +385,182 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     }
 }
 
+// ------------------------------------------------------- fused head, pipelined (N = 128, L = 16)
+// head_fused_fwd_kernel runs its phases one after the other on all 8 waves: the feature stream
+// (outconv, 26.5 us of its 35.7 at bs 32 x 128^2 x 64 channels), then Weff / GEMM / y0 / the
+// trace update (9 us of latency chains) - with one block per CU nothing overlaps that tail.  Here
+// 12 waves split the roles:
+//   waves 0..7 (streamers, the serial kernel's outconv configuration and per-CU stream rate): one
+//     continuous stream over the 17 rows in the order row 0, i0 .. i0+15, 256 pixels per pass with
+//     the next pass's loads issued before the current pass is reduced - so the block barriers
+//     between phases (every 2 passes = 4 rows) do not drain the memory pipeline;
+//   waves 8..11 (workers): phase 0 builds Weff = w + alpha (.) H_b in LDS; after every phase they
+//     form Y = X Weff for the 4 rows just streamed (thread = (column j, row pair), one k-ordered
+//     fmaf chain per row - the MFMA's chain, bit-identical), sigmoid, store; the phase after row 0's
+//     y0 runs the block's trace update.
+// What is left after the stream is one row's GEMM.  Arithmetic identical to head_fused_fwd_kernel
+// (the same outconv lane tree, k order, sigmoid and trace expressions).
+#ifndef PU_HP_SW
+#define PU_HP_SW 8
+#endif
+#ifndef PU_HP_ROT
+#define PU_HP_ROT 1
+#endif
+constexpr int HP_SW = PU_HP_SW * 64, HP_NT = HP_SW + 256, HP_U = 8, HP_N = 128;
+template <typename T>
+__global__ __launch_bounds__(HP_NT) void head_pipe_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ wo,
+                                                              const float* __restrict__ bo, int C,
+                                                              const float* __restrict__ H, const float* __restrict__ w,
+                                                              const float* __restrict__ alpha,
+                                                              const float* __restrict__ eta_p, float* __restrict__ X,
+                                                              float* __restrict__ Y, float* __restrict__ Hn, int rule) {
+#pragma clang fp contract(off)
+    constexpr int N = HP_N, L = 16, R = 16;
+    constexpr int PPP = HP_SW / L;            // pixels per lane-group round
+    constexpr int PPI = HP_U * PPP;           // pixels per pass
+    constexpr int NPIX = (R + 1) * N;         // the stream: row 0, then rows i0 .. i0+15
+    constexpr int NPASS = (NPIX + PPI - 1) / PPI;
+    constexpr int NPH = (NPASS + 1) / 2;      // phases (2 passes each)
+    constexpr int RPP = 2 * PPI / N;          // stream rows per phase (4 with 8 streamer waves)
+    constexpr int RPT = RPP / 2;              // rows per worker thread and phase
+    static_assert(PPI % N == 0 && RPT <= 3, "a pass is whole rows");
+    __shared__ __attribute__((aligned(16))) float xs[(R + 1) * N];   // stream order: row 0, then own rows
+    __shared__ __attribute__((aligned(16))) float ws[N * N];
+    __shared__ float y0s[N];
+    const int b = blockIdx.y;
+    const int i0 = blockIdx.x * R;
+    const int tid = threadIdx.x;
+    const bool streamer = tid < HP_SW;        // wave-uniform
+    const long long nn = (long long)N * N;
+    const T* fb = feat + (long long)b * nn * C;
+    const float* Hb = H + (long long)b * nn;
+
+    if (streamer) {
+        const float bias = bo ? bo[0] : 0.f;
+        const int lane = tid % L;
+        // column rotation per block: the 256 blocks' streams start at staggered addresses
+        const int rot = PU_HP_ROT ? (int)((blockIdx.x * 8 + blockIdx.y) * 37u) & (N - 1) : 0;
+        f32x4 buf[2][HP_U];
+        // pixels of pass k (stream order q -> image row: q / N == 0 ? 0 : i0 + q / N - 1)
+        auto load = [&](int k, f32x4 (&v)[HP_U]) {
+#pragma unroll
+            for (int u = 0; u < HP_U; ++u) {
+                const int q = min(k * PPI + tid / L + u * PPP, NPIX - 1);
+                const int r = q / N, col = (q + rot) & (N - 1);
+                const T* px = fb + ((long long)(r == 0 ? 0 : i0 + r - 1) * N + col) * C;
+                v[u] = fh_ld4<T>(px + lane * 4);
+            }
+        };
+        const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + lane * 4);
+        // reduce pass k from registers v (the next pass's loads already in flight)
+        auto reduce = [&](int k, const f32x4 (&v)[HP_U]) {
+#pragma unroll
+            for (int u = 0; u < HP_U; ++u) {
+                const int q = k * PPI + tid / L + u * PPP;
+                float sacc = 0.f;
+                sacc += dot4_fma(v[u], ww);
+                if (C > 4 * L) {                  // channels beyond the first 64 (not prefetched)
+                    const int qc = min(q, NPIX - 1);
+                    const int r = qc / N, col = (qc + rot) & (N - 1);
+                    const T* px = fb + ((long long)(r == 0 ? 0 : i0 + r - 1) * N + col) * C;
+                    for (int c = lane * 4 + 4 * L; c < C; c += 4 * L)
+                        sacc += dot4_fma(fh_ld4<T>(px + c), *reinterpret_cast<const f32x4*>(wo + c));
+                }
+                float t = sacc;
+                t += __shfl_xor(t, 8, 16);
+                t += __shfl_xor(t, 4, 16);
+                t += __shfl_xor(t, 2, 16);
+                t += __shfl_xor(t, 1, 16);
+                if (lane == 0 && q < NPIX) xs[(q & ~(N - 1)) + ((q + rot) & (N - 1))] = t + bias;
+            }
+        };
+        // passes in pairs (static buffer roles): a phase = 2 passes = 4 rows, then the barrier
+        load(0, buf[0]);
+#pragma unroll 1
+        for (int k = 0; k < NPASS; k += 2) {
+            if (k + 1 < NPASS) load(k + 1, buf[1]);
+            reduce(k, buf[0]);
+            if (k + 1 < NPASS) {
+                if (k + 2 < NPASS) load(k + 2, buf[0]);
+                reduce(k + 1, buf[1]);
+            }
+            __syncthreads();                  // this phase's rows are in xs
+        }
+        // X rows out (stream rows 1 .. 16 = image rows i0 .. i0+15)
+        for (int e = tid; e < R * N; e += HP_SW) X[(long long)b * nn + (long long)i0 * N + e] = xs[N + e];
+    } else {
+        const int tw = tid - HP_SW;           // 0 .. 255
+        const int j = tw & (N - 1), rh = tw >> 7;
+        // phase 0: Weff
+        {
+            const f32x4* w4 = reinterpret_cast<const f32x4*>(w);
+            const f32x4* a4 = reinterpret_cast<const f32x4*>(alpha);
+            const f32x4* h4 = reinterpret_cast<const f32x4*>(Hb);
+            for (int e0 = tw; e0 < N * N / 4; e0 += 8 * 256) {
+                f32x4 wv[8], av[8], hv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int o = e0 + 256 * u;
+                    wv[u] = w4[o]; av[u] = a4[o]; hv[u] = h4[o];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    f32x4 o;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[c] = wv[u][c] + av[u][c] * hv[u][c];   // torch: w + mul(alpha, hebb)
+                    reinterpret_cast<f32x4*>(ws)[e0 + 256 * u] = o;
+                }
+            }
+        }
+        for (int ph = 0; ph < NPH; ++ph) {
+            __syncthreads();                  // phase ph's stream rows are in xs
+            // Y of stream rows RPP ph + RPT rh .. (stream row 0 = image row 0 -> y0 only)
+            const int s0 = RPP * ph + RPT * rh;
+            const int nrow = max(0, min(RPT, R + 1 - s0));
+            if (nrow > 0) {
+                float acc[RPT];
+#pragma unroll
+                for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+                for (int k = 0; k < N; k += 4) {
+                    float wk[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) wk[e] = ws[(k + e) * N + j];
+#pragma unroll
+                    for (int r = 0; r < RPT; ++r)
+                        if (r < nrow) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) acc[r] = fmaf(xs[(s0 + r) * N + k + e], wk[e], acc[r]);
+                        }
+                }
+#pragma unroll
+                for (int r = 0; r < RPT; ++r)
+                    if (r < nrow) {
+                        const float y = 1.f / (1.f + expf(-acc[r]));
+                        if (s0 + r == 0) y0s[j] = y;
+                        else Y[((long long)b * N + i0 + s0 + r - 1) * N + j] = y;
+                    }
+            }
+            if (ph == 1) {                    // (RPP >= 2: y0 was formed in phase 0)
+                // trace update of rows i0 .. i0+15 (y0 formed in phase 0's GEMM - complete at this
+                // phase's barrier -, x0 = stream row 0)
+                const float eta = eta_p[0];
+                const float one_m_eta = 1.f - eta;
+                const f32x4* Hr = reinterpret_cast<const f32x4*>(Hb + (long long)i0 * N);
+                f32x4* Hnr = reinterpret_cast<f32x4*>(Hn + (long long)b * nn + (long long)i0 * N);
+                for (int e4 = tw; e4 < R * N / 4; e4 += 256) {
+                    const f32x4 h = Hr[e4];
+                    const int kk = (4 * e4) / N, jj = 4 * e4 - kk * N;
+                    const float x0 = xs[i0 + kk];
+                    f32x4 o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = trace_rule(h[e], x0, y0s[jj + e], eta, one_m_eta, rule);
+                    Hnr[e4] = o;
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------- backward
 // G = dy * (1 - y) * y   (ATen sigmoid_backward: grad * (1 - out) * out)
 __device__ __forceinline__ float sig_bwd(float dy, float y) {
@@ -652,6 +828,22 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
                "pu_plastic_head_fwd: hebb / w / alpha / hebb_out must be 16-byte aligned");
     const int q = C / 4;
     const int L = q >= 16 ? 16 : (q & (q - 1)) == 0 ? q : 16;    // lanes per pixel
+    // the pipelined kernel: N = 128, L = 16 lanes per pixel, the fused trace update
+    // (PU_HEAD_PIPE=0 keeps the phase-serial kernel: A/B runs)
+    static const bool pipe_on = [] {
+        const char* e = getenv("PU_HEAD_PIPE");
+        return !(e && e[0] == '0');
+    }();
+    if (pipe_on && N == HP_N && L == 16 && a->hebb_out) {
+        const dim3 pg(N / 16, a->batch);
+        if (a->feat_bf16)
+            hipLaunchKernelGGL((head_pipe_fwd_kernel<__bf16>), pg, dim3(HP_NT), 0, as_stream(stream), (const __bf16*)a->feat,
+                               a->out_w, a->out_b, C, a->hebb, a->w, a->alpha, a->eta, a->x, a->y, a->hebb_out, a->rule);
+        else
+            hipLaunchKernelGGL((head_pipe_fwd_kernel<float>), pg, dim3(HP_NT), 0, as_stream(stream), (const float*)a->feat,
+                               a->out_w, a->out_b, C, a->hebb, a->w, a->alpha, a->eta, a->x, a->y, a->hebb_out, a->rule);
+        return check_launch("pu_plastic_head_fwd");
+    }
     const int kc = fused_head_chunk(N);                           // Weff rows per LDS chunk
     size_t lds = ((size_t)(FH_R + 1) * N + (size_t)kc * N + N) * sizeof(float);
     if (lds < (size_t)PU_FH_LDS_MIN) lds = PU_FH_LDS_MIN;

@@ -1468,6 +1468,46 @@ __global__ void wgrad_sum_splits_kernel(const float* __restrict__ slab, int spli
     part[(long long)g * total + idx] = (s0 + s1) + (s2 + s3);
 }
 
+// pass 1 on float4 quads (total % 4 == 0): the same 4 chains per entry in the same order (so
+// bit-identical to wgrad_sum_splits_kernel), with two chain rounds' 8 x 16-B loads issued before
+// their adds - the scalar form kept 4 x 4 B per thread in flight and ran at ~1.3 TB/s.
+__global__ __launch_bounds__(256) void wgrad_sum_splits4_kernel(const float* __restrict__ slab, int splits,
+                                                                long long total, int G, double* __restrict__ part) {
+    const long long idx = 4 * (blockIdx.x * (long long)blockDim.x + threadIdx.x);
+    if (idx >= total) return;
+    const int g = blockIdx.y;
+    double s[4][4] = {};
+    const float* sp = slab + idx;
+    int z = g;
+    for (; z + 7 * G < splits; z += 8 * G) {
+        f32x4 v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = *reinterpret_cast<const f32x4*>(sp + (long long)(z + c * G) * total);
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[c & 3][e] += (double)v[c][e];
+    }
+    if (z + 3 * G < splits) {
+        f32x4 v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const f32x4*>(sp + (long long)(z + c * G) * total);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[c][e] += (double)v[c][e];
+        z += 4 * G;
+    }
+    for (; z < splits; z += G) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(sp + (long long)z * total);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[0][e] += (double)v[e];
+    }
+    double* o = part + (long long)g * total + idx;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (s[0][e] + s[1][e]) + (s[2][e] + s[3][e]);
+}
+
 // pass 2: sum the G groups (fixed order, fp64) and scatter to PyTorch's [n][c][kh][kw] + bias.
 // Threads [0, total) handle slab entries; threads [total, total + C) the ConvT bias (mode 2).
 // T = double: the G pass-1 partials;  T = float: the slab itself (G = splits, single pass).
@@ -2211,10 +2251,10 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
     const dim3 fgrid((unsigned)((threads + 255) / 256));
     const int taps = a->kh * a->kw;
-    // one launch for many splits of a few-thousand-entry slab (the direct small-channel / stem
-    // kernels, and the Winograd-domain kernel's 64 x 64 blocks at the 128^2 / 64^2 levels: 64-256
-    // splits), instead of the two-pass grouped form
-    if ((pl.small || pl.stem || (pl.wino && pl.splits >= 32)) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
+    // one launch for up to 1024 splits of a few-thousand-entry slab (the direct small-channel /
+    // stem kernels; measured slower than the two-pass grouped form on the Winograd-domain
+    // kernel's 64-256 splits: 0.37 vs 0.32 ms per C2 step)
+    if ((pl.small || pl.stem) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
         hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)ceil_div(total, (long long)WR_E)), dim3(256), 0, s,
                            (const float*)workspace, pl.splits, total, a->n, pl.Kcp, pl.K, pl.C, a->kh, a->kw,
                            a->bias_mode, a->dweight, a->dbias, a->accumulate);
@@ -2228,8 +2268,8 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
                                pl.Nr, pl.Kcp, pl.K, pl.C, taps, a->bias_mode, a->dweight, a->dbias, a->accumulate);
         } else {
             double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
-            hipLaunchKernelGGL(wgrad_sum_splits_kernel, dim3((unsigned)((total + 255) / 256), pl.G), dim3(256), 0, s,
-                               (const float*)workspace, pl.splits, total, pl.G, part);
+            hipLaunchKernelGGL(wgrad_sum_splits4_kernel, dim3((unsigned)((total / 4 + 255) / 256), pl.G), dim3(256), 0,
+                               s, (const float*)workspace, pl.splits, total, pl.G, part);
             hipLaunchKernelGGL(wgrad_finish_t_kernel<double>, tgrid, tblock, 0, s, (const double*)part, pl.G, pl.Nr,
                                pl.Kcp, pl.K, pl.C, taps, a->bias_mode, a->dweight, a->dbias, a->accumulate);
         }

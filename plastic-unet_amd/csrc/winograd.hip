@@ -472,59 +472,81 @@ struct WinoPackBatch {
     int count;
 };
 
+// Block = 32 output rows n x 64 reduced channels c (4 chunks) of one job.  The weights of the tile
+// are staged through LDS with coalesced reads (fwd: 32 rows of 64 x 9 contiguous floats; dgrad:
+// 64 rows of 32 x 9), so the thread that forms (n, 8 channels) reads its 72 values from LDS rather
+// than 288 scattered bytes of global memory; thread = (chunk, n, half): a wave's 16-byte stores of
+// one (chunk, position, plane) cover 32 n x 32 B = 1 KB contiguous.
+constexpr int WP_N = 32, WP_C = 64;
+constexpr int WP_LD = WP_C * 9 + 1;     // LDS floats per n row (+1: rows on distinct banks)
 __global__ __launch_bounds__(256) void wino_pack_kernel(const WinoPackBatch bt) {
 #pragma clang fp contract(off)
+    __shared__ float gw[WP_N * WP_LD];
     int j = 0, b0 = 0;
     while (j + 1 < bt.count && (int)blockIdx.x >= b0 + bt.job[j].blocks) b0 += bt.job[j++].blocks;
     const WinoPackJob J = bt.job[j];
-    // thread = (row a of G g G^T, chunk, n, half), a slowest: neighbouring lanes write
-    // neighbouring 16-byte halves of one 32-byte U row, so every store instruction covers a
-    // contiguous 1 KB; one row per thread keeps ~100 VGPRs (4 rows per thread: 244, 2 waves per
-    // SIMD - too few loads in flight, 2.3 TB/s)
-    const int idx = ((int)blockIdx.x - b0) * 256 + threadIdx.x;
-    const int c8s = J.c / 8;
-    const int per_a = J.n * c8s;
-    if (idx >= 4 * per_a) return;
-    const int a = idx / per_a;
-    const int rest = idx - a * per_a;
-    const int nh = rest >> 1;
-    const int n = nh % J.n;
-    const int c8 = (nh / J.n) * 2 + (rest & 1);
-    typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
-    const int chunk = c8 >> 1, half = c8 & 1;
-    bf16x8v o[4][3];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int c = c8 * 8 + e;
-        double g[3][3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int s = 0; s < 3; ++s)
-                g[r][s] = J.dgrad ? (double)J.w[(((long long)c * J.n + n) * 3 + (2 - r)) * 3 + (2 - s)]
-                                  : (double)J.w[(((long long)n * J.c + c) * 3 + r) * 3 + s];
-        double t[3];   // row a of G g
-#pragma unroll
-        for (int s = 0; s < 3; ++s)
-            t[s] = a == 0 ? g[0][s] : a == 1 ? 0.5 * (g[0][s] + g[1][s] + g[2][s])
-                 : a == 2 ? 0.5 * (g[0][s] - g[1][s] + g[2][s]) : g[2][s];
-        const double u[4] = {t[0], 0.5 * (t[0] + t[1] + t[2]), 0.5 * (t[0] - t[1] + t[2]), t[2]};
-#pragma unroll
-        for (int bc = 0; bc < 4; ++bc) {
-            const float x = (float)u[bc];
-            const __bf16 h = (__bf16)x;
-            const float rr = x - (float)h;
-            const __bf16 mm = (__bf16)rr;
-            o[bc][0][e] = h;
-            o[bc][1][e] = mm;
-            o[bc][2][e] = (__bf16)(rr - (float)mm);
+    const int blk = (int)blockIdx.x - b0;
+    const int nblks = (J.n + WP_N - 1) / WP_N;
+    const int n0 = (blk % nblks) * WP_N, c0 = (blk / nblks) * WP_C;
+    const int nn = min(WP_N, J.n - n0), cc = min(WP_C, J.c - c0);
+    const int tid = threadIdx.x;
+    // stage g[n][c][3][3] (dgrad: g[r][s] = w[c][n][2-r][2-s], flipped when read below)
+    if (!J.dgrad) {
+        for (int e = tid; e < WP_N * WP_C * 9; e += 256) {
+            const int nl = e / (WP_C * 9), rest = e - nl * WP_C * 9;
+            if (nl < nn && rest < cc * 9) gw[nl * WP_LD + rest] = J.w[((long long)(n0 + nl) * J.c + c0) * 9 + rest];
+        }
+    } else {
+        for (int e = tid; e < WP_C * WP_N * 9; e += 256) {
+            const int cl = e / (WP_N * 9), rest = e - cl * WP_N * 9;
+            const int nl = rest / 9, k = rest - nl * 9;
+            if (cl < cc && nl < nn) gw[nl * WP_LD + cl * 9 + k] = J.w[((long long)(c0 + cl) * J.n + n0) * 9 + rest];
         }
     }
+    __syncthreads();
+    const int half = tid & 1, nl = (tid >> 1) & 31, ch = tid >> 6;
+    const int c8 = (c0 >> 3) + ch * 2 + half;
+    if (nl >= nn || ch * 16 + half * 8 >= cc) return;
+    const int n = n0 + nl;
+    const int chunk = c8 >> 1;
+    typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+    const float* gr = gw + nl * WP_LD + (ch * 16 + half * 8) * 9;
+    // one row a of G g G^T at a time (12 output vectors live)
+#pragma unroll 1
+    for (int a = 0; a < 4; ++a) {
+        asm volatile("" ::: "memory");        // re-read g from LDS per row (no 72 hoisted doubles)
+        bf16x8v o[4][3];
 #pragma unroll
-    for (int bc = 0; bc < 4; ++bc)
+        for (int e = 0; e < 8; ++e) {
+            double g[3][3];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-            *reinterpret_cast<bf16x8v*>(J.out + ((((long long)chunk * 16 + a * 4 + bc) * 3 + pl) * J.n + n) * 16 + half * 8) = o[bc][pl];
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int s = 0; s < 3; ++s)
+                    g[r][s] = J.dgrad ? (double)gr[e * 9 + (2 - r) * 3 + (2 - s)] : (double)gr[e * 9 + r * 3 + s];
+            double t[3];   // row a of G g
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+                t[s] = a == 0 ? g[0][s] : a == 1 ? 0.5 * (g[0][s] + g[1][s] + g[2][s])
+                     : a == 2 ? 0.5 * (g[0][s] - g[1][s] + g[2][s]) : g[2][s];
+            const double u[4] = {t[0], 0.5 * (t[0] + t[1] + t[2]), 0.5 * (t[0] - t[1] + t[2]), t[2]};
+#pragma unroll
+            for (int bc = 0; bc < 4; ++bc) {
+                const float x = (float)u[bc];
+                const __bf16 h = (__bf16)x;
+                const float rr = x - (float)h;
+                const __bf16 mm = (__bf16)rr;
+                o[bc][0][e] = h;
+                o[bc][1][e] = mm;
+                o[bc][2][e] = (__bf16)(rr - (float)mm);
+            }
+        }
+#pragma unroll
+        for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                *reinterpret_cast<bf16x8v*>(J.out + ((((long long)chunk * 16 + a * 4 + bc) * 3 + pl) * J.n + n) * 16 + half * 8) = o[bc][pl];
+    }
 }
 
 // host side -------------------------------------------------------------------------------------
@@ -638,7 +660,7 @@ extern "C" int pu_pack_wino(const pu_wino_job* jobs, int n_jobs, void* stream) {
             o.n = n;
             o.c = c;
             o.dgrad = J.dgrad != 0;
-            o.blocks = ceil_div(4LL * n * (c / 8), 256);   // one thread per (row a, n, 8 channels)
+            o.blocks = ceil_div(n, WP_N) * ceil_div(c, WP_C);   // 32 n x 64 c tiles
             total += o.blocks;
         }
         hipLaunchKernelGGL(wino_pack_kernel, dim3((unsigned)total), dim3(256), 0, as_stream(stream), b);

@@ -30,12 +30,15 @@ def eval_net(net, X_val, y_val, device, criterion=None, debug=False, batch=32):
             B = xb.shape[0]
             hebb = net.initialZeroHebb(B)          # zero trace per slot; the update is discarded
             y, _ = net(xb, hebb)
+            yf, tf = y.reshape(B, -1), tb.reshape(B, -1)
+            losses = torch.stack([criterion(yf[b], tf[b]) if criterion is not None else bce_loss(yf[b], tf[b])
+                                  for b in range(B)])
+            # one device->host copy per chunk; the per-sample sums in the reference's order
+            for b, l in enumerate(losses.cpu().tolist()):
+                total_loss += l
+            y_np, t_np = yf.cpu().numpy(), tf.cpu().numpy()
             for b in range(B):
-                yf = y[b].reshape(-1)
-                tf = tb[b].reshape(-1)
-                loss = criterion(yf, tf) if criterion is not None else bce_loss(yf, tf)
-                total_loss += loss.item()
-                total_acc += fast_iou_metric(y_true_in=tf.cpu().numpy(), y_pred_in=yf.cpu().numpy())
+                total_acc += fast_iou_metric(y_true_in=t_np[b], y_pred_in=y_np[b])
     return total_acc / n, total_loss / n
 
 
