@@ -191,7 +191,7 @@ typedef struct {
 
 size_t pu_wgrad_workspace_bytes(const pu_wgrad_args* a);
 /* the tile (bn x bk), loader (qvec: 0 scalar, 1 float4, 2 small-channel direct kernel, 3 halo-reuse kernel,
- * 4 stem kernel, 5 Winograd-domain kernel) and
+ * 4 stem kernel, 5 Winograd-domain kernel, 6 pointwise small-channel kernel) and
  * pixel-row split count pu_wgrad would use */
 int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec, int* splits);
 int pu_wgrad(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);
@@ -308,7 +308,7 @@ int pu_outconv_bwd(const float* x, const float* w, const float* dy, float* dx, f
 int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream);
 size_t pu_conv_igemm_bf16_workspace_bytes(const pu_conv_args* a);
 /* the bf16 kernel pu_conv_igemm_bf16 would launch: tile bm x bn, K splits, kind 0 = tile kernel,
- * 1 = lean per-tap kernel, 2 = halo kernel (kind may be NULL) */
+ * 1 = lean per-tap kernel, 2 = halo kernel, 3 = row-stream kernel (kind may be NULL) */
 int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, int* ksplit, int* kind);
 size_t pu_wgrad_bf16_workspace_bytes(const pu_wgrad_args* a);
 int pu_wgrad_bf16(const pu_wgrad_args* a, void* workspace, size_t workspace_bytes, void* stream);

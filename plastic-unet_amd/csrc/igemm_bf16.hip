@@ -941,6 +941,182 @@ __global__ __launch_bounds__(H2_NT) void igemm_bf16_halo2_kernel(const IgemmBf16
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing (dead) loads drain before exit
 }
 
+// ---------------------------------------------------------------- row-stream bf16 kernel
+// The 128-wide, 64 -> 64 channel 3x3 convolutions of config C3's top level (inc.conv2 and
+// up4.conv2, fwd and dgrad: 4 of the 6 top-level launches, ~77 us each on the halo kernel at 0.2 of
+// the MFMA peak).  The halo kernel re-loads the 36.9 KB of a 32-channel group's weights for every
+// 256-pixel tile and its (R+2)/R = 2x halo; here a block keeps ALL 9 x 64 x 64 weights resident in
+// LDS (72 KB, loaded once) and walks a strip of 16 output rows of one image, one row per step:
+// input rows stream through a 5-row LDS ring by LDS-DMA (16 KB per row, issued two steps ahead),
+// so each input byte is fetched once per strip and the per-row work is 72 MFMAs per wave.
+//   block: 4 waves (one per SIMD, one block per CU: 153 KB of LDS), wave = 32 pixels x 64 output
+//     channels (2 fragments; 1 pixel + 2 weight fragment reads per 2 MFMAs), fragment reads two
+//     k-steps ahead;
+//   LDS images: 128-byte rows (64 bf16 channels) with 16-byte chunk c stored at c ^ ((row >> 1) & 7)
+//     (conflict-free ds_read_b128 for 32 consecutive rows at any shift; the DMA lanes pick their
+//     source chunk accordingly), ring rows of 130 pixels whose two padding pixels stay zero;
+//   epilogue: bias preloaded once, mask / residual / accumulate operands of the row loaded at the
+//     start of its step (they land under its MFMAs), 8-byte stores.
+// K order (32-channel group, tap, 16-channel half) and the MFMA sequence per accumulator are
+// igemm_bf16_halo_kernel's, so the two are bit-identical.  Host: rows_ok_b.
+constexpr int RS_W = 128, RS_ROWS = 16, RS_RING = 5;
+constexpr int RS_ROWB = (RS_W + 2) * 128;                        // 16640 B per ring row
+constexpr int RS_WB = 9 * 64 * 128;                              // 73728 B of weights
+constexpr int RS_LDS = RS_RING * RS_ROWB + RS_WB;                // 156928 B
+
+__global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Params p) {
+    extern __shared__ __attribute__((aligned(1024))) char rs_lds[];
+    char* const wl = rs_lds + RS_RING * RS_ROWB;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+    const int strips = p.Ho / RS_ROWS;
+    const int b = blockIdx.x / strips;
+    const int r0 = (blockIdx.x - b * strips) * RS_ROWS;
+    const unsigned xbytes = (unsigned)p.in_pix * 128u;           // 64 bf16 channels per pixel
+    const unsigned wbytes = (unsigned)(64 * p.k_pad * 2);
+
+    // padding pixels 0 and 129 of every ring row: zero, never written by the DMA
+    if (tid < RS_RING * 2 * 8) {
+        const int row = tid >> 4, side = (tid >> 3) & 1, ch = tid & 7;
+        *reinterpret_cast<f32x4*>(rs_lds + row * RS_ROWB + side * (RS_W + 1) * 128 + ch * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // weights [tap][n][64 channels] (chunk-swizzled by n), 72 x 1 KB, 18 per wave
+#pragma unroll
+    for (int j = 0; j < 18; ++j) {
+        const int I = wave + 4 * j;
+        const int row = I * 8 + (lane >> 3);
+        const int tap = row >> 6, n = row & 63;
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const unsigned vo = (unsigned)(n * p.k_pad + (c >> 2) * 288 + tap * 32 + (c & 3) * 8) * 2u;
+        lean_load(p.wt, wbytes, wl + I * 1024, vo, 0u);
+    }
+    // input row ir of image b -> ring slot (ir + 1) % RS_RING, pixels 1 .. 128 (4 x 1 KB per wave)
+    unsigned xvo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int I = wave + 4 * j;
+        const int col = I * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (((col + 1) >> 1) & 7);
+        xvo[j] = (unsigned)(col * 64 + c * 8) * 2u;
+    }
+    auto load_row = [&](int ir) {
+        const bool ok = ir >= r0 - 1 && ir <= r0 + RS_ROWS && (unsigned)ir < (unsigned)p.Hi;
+        char* base = rs_lds + ((ir + 1) % RS_RING) * RS_ROWB + 128;
+        const unsigned soff = ok ? (unsigned)((b * p.Hi + ir) * RS_W) * 128u : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lean_load(p.src0, ok ? xbytes : 0u, base + (wave + 4 * j) * 1024, xvo[j], soff);
+    };
+    load_row(r0 - 1);
+    load_row(r0);
+    load_row(r0 + 1);
+    load_row(r0 + 2);
+
+    // per-lane fragment offsets: pixel fragment (tap column ts, 16-channel step u), weight (u)
+    const int q0 = wave * 32;
+    unsigned xoff[3][4], woff[4];
+#pragma unroll
+    for (int ts = 0; ts < 3; ++ts) {
+        const int pl = q0 + lr + ts;                              // ring pixel (col + 1)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) xoff[ts][u] = (unsigned)(pl * 128 + (((2 * u + lh) ^ ((pl >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) woff[u] = (unsigned)(lr * 128 + (((2 * u + lh) ^ ((lr >> 1) & 7)) << 4));
+
+    // bias of this lane's 8 channel quads (n = j*32 + 8q + 4lh)
+    f32x4 bias4[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            bias4[j][q] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + j * 32 + 8 * q + 4 * lh) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool has_m = p.mask0 != nullptr, has_r = p.resid != nullptr, has_a = (p.flags & PU_EPI_ACCUM) != 0;
+    const int E = 8 * ((has_m ? 1 : 0) + (has_r ? 1 : 0) + (has_a ? 1 : 0));
+
+    for (int r = r0; r < r0 + RS_ROWS; ++r) {
+        // input row r+1 landed (issued two steps ago; later: stores, the epilogue loads and one row)
+        if (r == r0) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");   // + the padding zeros
+        else if (r == r0 + 1) wait_vm_plus<12>(E);
+        else wait_vm_plus<20>(E);
+        __builtin_amdgcn_s_barrier();                             // ... for every wave; slot of row r-2 free
+        asm volatile("" ::: "memory");
+        const long long m = (long long)(b * p.Ho + r) * RS_W + q0 + lr;
+        bf16x4 mv[2][4], rv[2][4], av[2][4];
+        if (E) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const long long off = m * 64 + j * 32 + 8 * q + 4 * lh;
+                    if (has_m) mv[j][q] = *reinterpret_cast<const bf16x4*>(p.mask0 + off);
+                    if (has_r) rv[j][q] = *reinterpret_cast<const bf16x4*>(p.resid + off);
+                    if (has_a) av[j][q] = *reinterpret_cast<const bf16x4*>(p.dst0 + off);
+                }
+        }
+        load_row(r + 3);
+
+        const int sb[3] = {(r % RS_RING) * RS_ROWB, ((r + 1) % RS_RING) * RS_ROWB, ((r + 2) % RS_RING) * RS_ROWB};
+        f32x16 acc[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+        bf16x8 fx[3], fw[3][2];
+        auto rd = [&](auto S) {
+            constexpr int s = decltype(S)::value;
+            constexpr int g = s / 18, t = (s % 18) / 2, kk = s % 2, u = g * 2 + kk;
+            fx[s % 3] = *reinterpret_cast<const bf16x8*>(rs_lds + sb[t / 3] + xoff[t % 3][u]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                fw[s % 3][j] = *reinterpret_cast<const bf16x8*>(wl + (t * 64 + j * 32) * 128 + woff[u]);
+        };
+        rd(std::integral_constant<int, 0>{});
+        rd(std::integral_constant<int, 1>{});
+        static_for<36>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            if constexpr (s + 2 < 36) rd(std::integral_constant<int, s + 2>{});
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[s % 3][j], fx[s % 3], acc[j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");         // this row's epilogue operands
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[j][4 * q + e];
+                if (p.bias) v += bias4[j][q];
+                if (has_r) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += (float)rv[j][q][e];
+                }
+                if (p.flags & PU_EPI_RELU) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                }
+                if (has_m) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) if (!((float)mv[j][q][e] > 0.f)) v[e] = 0.f;
+                }
+                if (has_a) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += (float)av[j][q][e];
+                }
+                bf16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+                *reinterpret_cast<bf16x4*>(p.dst0 + m * 64 + j * 32 + 8 * q + 4 * lh) = o;
+            }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // the trailing (empty) row loads drain
+}
+
 __global__ __launch_bounds__(256) void igemm_bf16_splitk_epilogue_kernel(const IgemmBf16Params p) {
     const int nq = p.N >> 2;
     const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -1015,6 +1191,20 @@ static bool halo2_ok_b(const pu_conv_args* a) {
                          (uintptr_t)a->resid;
     return halo_ok_b(a) && (a->flags & PU_CONV_HALO_DMA) && a->out_h % (512 / a->out_w) == 0 && a->n0 % 8 == 0 &&
            (ae & 15) == 0;
+}
+
+// the row-stream kernel: the halo kernel's 3x3 / s1 / p1 shapes restricted to width 128, one
+// 64-channel source, 64 output channels into one destination, 16-row strips; PU_BF16_ROWS=0 keeps
+// the halo kernel (A/B runs)
+static bool rows_ok_b(const pu_conv_args* a) {
+    static const bool on = [] {
+        const char* e = getenv("PU_BF16_ROWS");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || !halo_ok_b(a) || (a->flags & PU_CONV_HALO_DMA)) return false;   // the DMA ring when opted in
+    if (a->out_w != RS_W || a->out_h % RS_ROWS || a->c0 != 64 || a->c1 != 0 || a->n != 64) return false;
+    if (a->n0 != 0 && a->n0 != 64) return false;
+    return (long long)a->batch * a->in_h * a->in_w * 128 < (1LL << 31);
 }
 
 template <int W>
@@ -1127,6 +1317,13 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
     if (st != PU_OK) return st;
     const int N = a->n;
     hipStream_t s = as_stream(stream);
+    if (rows_ok_b(a)) {
+        p.ksplit = 1;
+        p.gn = 1;
+        const dim3 rgrid((unsigned)(a->batch * (a->out_h / RS_ROWS)));
+        hipLaunchKernelGGL(igemm_bf16_rows_kernel, rgrid, dim3(256), RS_LDS, s, p);
+        return check_launch("pu_conv_igemm_bf16 (rows)");
+    }
     if (halo2_ok_b(a)) {
         p.ksplit = 1;
         p.gn = N / H2_BN;
@@ -1188,6 +1385,13 @@ extern "C" int pu_conv_igemm_bf16_tile(const pu_conv_args* a, int* bm, int* bn, 
     int st = setup_bf16(a, &p, &M);
     if (st != PU_OK) return st;
     int ks, tp;
+    if (rows_ok_b(a)) {               // the row-stream kernel: one 128-pixel row x 64 channels per step
+        *bm = 128;
+        *bn = 64;
+        if (ksplit) *ksplit = 1;
+        if (kind) *kind = 3;
+        return PU_OK;
+    }
     if (halo2_ok_b(a)) {              // the DMA-ring halo kernel: 512 pixels x 64 channels
         *bm = 512;
         *bn = H2_BN;

@@ -1230,6 +1230,72 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(const WgradParams p) {
     }
 }
 
+// ------------------------------------------------------- pointwise (1x1) small weight gradient
+// dW[n][c] = sum_m dZ[m][n] X[m][c] and db[n] = sum_m dZ[m][n] for a 1x1 / s1 / p0 conv with a
+// handful of channels (config C4's CoordConv 1x1: 4 -> 8 channels at 256^2, 2.1 M pixels).  As a
+// GEMM it is K = 4: the tiled kernel spent 85 latency-bound 16-row stages per block on it (155 us
+// for 100 MB); here a thread streams whole pixels (C + N floats, consecutive pixels on consecutive
+// lanes) and keeps all N x (C + 1) sums in registers, fmaf chains in pixel order.  The block's 256
+// chains reduce in a fixed butterfly (xor 32 .. 1) then wave order, one slab row per block; the
+// fixed-order split reduction finishes it - deterministic.
+template <int C, int N>
+__global__ __launch_bounds__(256) void wgrad_pw_kernel(const WgradParams p) {
+    constexpr int V = N * (C + 1);                // C weights + the bias per output channel
+    __shared__ float part[4][V];
+    const int tid = threadIdx.x;
+    float acc[N][C + 1];
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int c = 0; c <= C; ++c) acc[n][c] = 0.f;
+    const long long m0 = (long long)blockIdx.x * p.mps;
+    const long long m1 = min((long long)p.M, m0 + p.mps);
+    for (long long m = m0 + tid; m < m1; m += 256) {
+        float x[C], g[N];
+        if constexpr (C % 4 == 0) {
+#pragma unroll
+            for (int q = 0; q < C / 4; ++q) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(p.src0 + m * C + 4 * q);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[4 * q + e] = v[e];
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = p.src0[m * C + c];
+        }
+#pragma unroll
+        for (int q = 0; q < N / 4; ++q) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(p.P + m * N + 4 * q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) g[4 * q + e] = v[e];
+        }
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) acc[n][c] = fmaf(g[n], x[c], acc[n][c]);
+            acc[n][C] += g[n];
+        }
+    }
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int c = 0; c <= C; ++c) {
+            float v = acc[n][c];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) part[wave][n * (C + 1) + c] = v;
+        }
+    __syncthreads();
+    float* slab = p.slab + (long long)blockIdx.x * p.Nr * p.Kcp;
+    for (int i = tid; i < V; i += 256) {
+        const float v = ((part[0][i] + part[1][i]) + part[2][i]) + part[3][i];
+        const int n = i / (C + 1), c = i - n * (C + 1);
+        if (c < C) slab[(long long)n * p.Kcp + c] = v;
+        else if (p.bias_mode == 1) slab[(long long)n * p.Kcp + p.K] = v;
+    }
+}
+
 // ------------------------------------------------------------- small-channel weight gradient
 // 3x3/s1/p1 with C <= 16 input and N <= 16 output channels (configs C4/C5's 8/16-channel levels):
 // a GEMM with N, K this small wastes most of an MFMA tile, so each block sweeps 16 x 32 pixel
@@ -1550,6 +1616,89 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
     }
 }
 
+// wgrad_finish_kernel on quads of 4 consecutive entries of one slab row (Kc % 4 == 0): the same
+// 4 fp64 chains per entry in the same order (bit-identical), 8 partial quads in flight per thread
+// instead of 4 scalars.  The ConvT bias (mode 2: entries t*C + c of row N over every tap t and
+// partial g) runs as 4 chains over the flattened (t, g) sequence with 8 loads in flight - the
+// scalar form's one dependent chain of taps x G loads was a latency tail (17.7 us for a 64-channel
+// ConvT in C2).
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_finish4_kernel(const T* __restrict__ part, int G, int Nr, int Kc, int N,
+                                                            int K, int C, int kh, int kw, int bias_mode,
+                                                            float* __restrict__ dw, float* __restrict__ db,
+                                                            int accumulate) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    const long long total = (long long)Nr * Kc;
+    const long long nq = total >> 2;
+    const long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (q < nq) {
+        const long long idx = 4 * q;
+        const int n = int(idx / Kc);
+        const int k0 = int(idx - (long long)n * Kc);
+        if (n >= N) return;
+        const T* sp = part + idx;
+        double s[4][4] = {};
+        int g = 0;
+        for (; g + 7 < G; g += 8) {
+            t4 v[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) v[c] = *reinterpret_cast<const t4*>(sp + (long long)(g + c) * total);
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s[c & 3][e] += (double)v[c][e];
+        }
+        if (g + 3 < G) {
+            t4 v[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const t4*>(sp + (long long)(g + c) * total);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s[c][e] += (double)v[c][e];
+            g += 4;
+        }
+        for (; g < G; ++g) {
+            const t4 v = *reinterpret_cast<const t4*>(sp + (long long)g * total);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[0][e] += (double)v[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int k = k0 + e;
+            const float v = (float)((s[0][e] + s[1][e]) + (s[2][e] + s[3][e]));
+            if (k < K) {
+                const int tap = k / C, c = k - tap * C;
+                const int r = tap / kw, ss = tap - r * kw;
+                float* o = dw + (((long long)n * C + c) * kh + r) * kw + ss;
+                *o = accumulate ? *o + v : v;
+            } else if (bias_mode == 1 && k == K) {
+                db[n] = accumulate ? db[n] + v : v;
+            }
+        }
+    } else if (bias_mode == 2 && q < nq + C) {
+        const int c = int(q - nq);
+        const int J = kh * kw * G;                       // j = t * G + g
+        const T* bp = part + (long long)N * Kc + c;
+        auto at = [&](int j) {
+            const int t = j / G, gg = j - t * G;
+            return (double)bp[(long long)gg * total + t * C];
+        };
+        double s[4] = {0.0, 0.0, 0.0, 0.0};
+        int j = 0;
+        for (; j + 7 < J; j += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = at(j + u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s[u & 3] += v[u];
+        }
+        for (; j < J; ++j) s[0] += at(j);
+        const float v = (float)((s[0] + s[1]) + (s[2] + s[3]));
+        db[c] = accumulate ? db[c] + v : v;
+    }
+}
+
 // pass 2 with coalesced stores: block (chunk of 256 channels, row n) sums slab[.][n][tap*C + c]
 // for its channels x taps (thread = (tap, 4 channels): 1-KB float4 reads per wave and split),
 // transposes through LDS and stores the contiguous [c][kh][kw] run of dweight[n] as float4 (the
@@ -1623,6 +1772,7 @@ struct WgradPlan {
     int BN, BK, splits, mps, Nr, Kc, Kcp, M, K, C, G, gx, gy;
     bool qvec, dma, small, halo, stem;
     bool wino = false;                        // Winograd-domain kernel (wgrad_wino_x6_kernel)
+    bool pw = false;                          // pointwise small-channel kernel (wgrad_pw_kernel)
     int tiles = 0, tps = 0;
     int nt = 1;                               // halo kernel: 64-channel output tiles per block
     int tiles_w, tiles_h;
@@ -1635,6 +1785,14 @@ static bool stem_wgrad_ok(const pu_wgrad_args* a) {
     return a->c0 == 1 && a->c1 == 0 && (a->n == 32 || a->n == 64) && a->kh == 3 && a->kw == 3 && a->stride == 1 &&
            a->pad == 1 && a->in_h == a->out_h && a->in_w == a->out_w && a->bias_mode == 1 &&
            ((uintptr_t)a->rows & 15) == 0;
+}
+
+// 1x1 / s1 / p0 same-size conv, one source, (C, N) an instantiated wgrad_pw_kernel pair
+static bool pw_wgrad_ok(const pu_wgrad_args* a) {
+    const int C = a->c0, N = a->n;
+    return a->c1 == 0 && a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad == 0 && a->in_h == a->out_h &&
+           a->in_w == a->out_w && a->bias_mode != 2 && (C == 3 || C == 4) && (N == 4 || N == 8 || N == 16) &&
+           (((uintptr_t)a->rows & 15) == 0) && (C % 4 || ((uintptr_t)a->src0 & 15) == 0);
 }
 
 static bool small_wgrad_ok(const pu_wgrad_args* a) {
@@ -1688,12 +1846,22 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     pl->qvec = (a->c0 % 4 == 0) && (a->c1 % 4 == 0);
     pl->small = small_wgrad_ok(a);
     pl->stem = stem_wgrad_ok(a);
+    pl->pw = pw_wgrad_ok(a);
     pl->halo = false;
     if (pl->qvec) {
         PU_REQUIRE(((uintptr_t)a->src0 & 15) == 0 && ((uintptr_t)a->src1 & 15) == 0, "pu_wgrad: sources must be 16-byte aligned");
     }
     PU_REQUIRE(((uintptr_t)a->rows & 15) == 0, "pu_wgrad: rows must be 16-byte aligned");
     pl->dma = pl->qvec;
+    if (pl->pw) {                      // pointwise: contiguous pixel ranges, one slab row block each
+        pl->splits = (int)(M / 256 < 1024 ? (M + 255) / 256 : 1024);
+        pl->mps = (int)ceil_div(M, (long long)pl->splits);
+        pl->splits = (int)ceil_div(M, (long long)pl->mps);
+        pl->BN = a->n; pl->BK = pl->K; pl->gx = pl->gy = 1; pl->dma = false;
+        pl->tiles_w = pl->tiles_h = 0;
+        plan_groups(pl);
+        return PU_OK;
+    }
     if (pl->small || pl->stem) {       // direct kernels: one slab row block per block
         pl->tiles_w = ceil_div(a->out_w, pl->stem ? SWS_TW : SW_TW);
         pl->tiles_h = ceil_div(a->out_h, pl->stem ? SWS_TH : SW_TH);
@@ -2254,7 +2422,7 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
     // one launch for up to 1024 splits of a few-thousand-entry slab (the direct small-channel /
     // stem kernels; measured slower than the two-pass grouped form on the Winograd-domain
     // kernel's 64-256 splits: 0.37 vs 0.32 ms per C2 step)
-    if ((pl.small || pl.stem) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
+    if ((pl.small || pl.stem || pl.pw) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
         hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)ceil_div(total, (long long)WR_E)), dim3(256), 0, s,
                            (const float*)workspace, pl.splits, total, a->n, pl.Kcp, pl.K, pl.C, a->kh, a->kw,
                            a->bias_mode, a->dweight, a->dbias, a->accumulate);
@@ -2272,6 +2440,23 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
                                s, (const float*)workspace, pl.splits, total, pl.G, part);
             hipLaunchKernelGGL(wgrad_finish_t_kernel<double>, tgrid, tblock, 0, s, (const double*)part, pl.G, pl.Nr,
                                pl.Kcp, pl.K, pl.C, taps, a->bias_mode, a->dweight, a->dbias, a->accumulate);
+        }
+        return check_launch("pu_wgrad (reduce)");
+    }
+    if (pl.Kcp % 4 == 0) {
+        const long long threads4 = total / 4 + (a->bias_mode == 2 ? pl.C : 0);
+        const dim3 grid4((unsigned)((threads4 + 255) / 256));
+        if (pl.G == 1) {
+            hipLaunchKernelGGL(wgrad_finish4_kernel<float>, grid4, dim3(256), 0, s, (const float*)workspace,
+                               pl.splits, pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight,
+                               a->dbias, a->accumulate);
+        } else {
+            double* part = (double*)((char*)workspace + ((pl.slab_bytes() + 255) / 256) * 256);
+            hipLaunchKernelGGL(wgrad_sum_splits4_kernel, dim3((unsigned)((total / 4 + 255) / 256), pl.G), dim3(256), 0,
+                               s, (const float*)workspace, pl.splits, total, pl.G, part);
+            hipLaunchKernelGGL(wgrad_finish4_kernel<double>, grid4, dim3(256), 0, s, (const double*)part, pl.G,
+                               pl.Nr, pl.Kcp, a->n, pl.K, pl.C, a->kh, a->kw, a->bias_mode, a->dweight, a->dbias,
+                               a->accumulate);
         }
         return check_launch("pu_wgrad (reduce)");
     }
@@ -2365,7 +2550,7 @@ extern "C" int pu_wgrad_tile(const pu_wgrad_args* a, int* bn, int* bk, int* qvec
     if (st != PU_OK) return st;
     if (bn) *bn = pl.BN;
     if (bk) *bk = pl.BK;
-    if (qvec) *qvec = pl.wino ? 5 : pl.stem ? 4 : pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo, 4: stem, 5: Winograd
+    if (qvec) *qvec = pl.pw ? 6 : pl.wino ? 5 : pl.stem ? 4 : pl.small ? 2 : pl.halo ? 3 : (pl.qvec ? 1 : 0);   // 2: small-channel direct, 3: halo, 4: stem, 5: Winograd, 6: pointwise
     if (splits) *splits = pl.splits;
     return PU_OK;
 }
@@ -2400,6 +2585,16 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
         if (a->n == 64) hipLaunchKernelGGL(wgrad_stem_kernel<64>, dim3(pl.splits), dim3(256), 0, s, p);
         else hipLaunchKernelGGL(wgrad_stem_kernel<32>, dim3(pl.splits), dim3(256), 0, s, p);
         st = check_launch("pu_wgrad (stem)");
+        if (st != PU_OK) return st;
+        phase &= ~1;
+    }
+    if (pl.pw && (phase & 1)) {
+        const int C = pl.C, N = a->n;
+        const dim3 sg(pl.splits);
+#define PU_PW(C_, N_) if (C == C_ && N == N_) hipLaunchKernelGGL((wgrad_pw_kernel<C_, N_>), sg, dim3(256), 0, s, p)
+        PU_PW(3, 4); else PU_PW(3, 8); else PU_PW(3, 16); else PU_PW(4, 4); else PU_PW(4, 8); else PU_PW(4, 16);
+#undef PU_PW
+        st = check_launch("pu_wgrad (pointwise)");
         if (st != PU_OK) return st;
         phase &= ~1;
     }

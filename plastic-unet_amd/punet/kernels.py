@@ -276,7 +276,7 @@ def _igemm_bf16(L, a, batch, out_hw, k, c0, c1, n, dst0):
     bm, bn, ks, kind = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     L.pu_conv_igemm_bf16_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(ks), ctypes.byref(kind))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "igemm_bf16<%dx%d%s%s>" % (bm.value, bn.value, ("", ",lean", ",halo")[kind.value],
+    tag = "igemm_bf16<%dx%d%s%s>" % (bm.value, bn.value, ("", ",lean", ",halo", ",rows")[kind.value],
                                      ",k%d" % ks.value if ks.value > 1 else "")
     with _Rec(tag, flops=2.0 * M * n * k * k * (c0 + c1)):
         check(L.pu_conv_igemm_bf16(ctypes.byref(a), _stream()), "pu_conv_igemm_bf16")
@@ -321,7 +321,7 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
     bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     L.pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp))
     M = batch * out_hw[0] * out_hw[1]
-    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct", "halo", "stem", "wino")[qv.value])
+    tag = "wgrad<%dx%d,%s>" % (bn.value, bk.value, ("scalar", "vec4", "direct", "halo", "stem", "wino", "pointwise")[qv.value])
     if a.math == 1 and qv.value in (1, 3, 5):
         tag = tag[:-1] + ",x6>"
     # the GEMM and the split reduction timed apart (they are separate kernels in rocprof too)
@@ -331,10 +331,12 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
         check(L.pu_wgrad_phase(ctypes.byref(a), ws.data_ptr(), nbytes, 2, _stream()), "pu_wgrad_phase")
 
 
-def wgrad_kind(*, batch, hw, n, c0, c1=0):
-    """Which kernel pu_wgrad takes for an fp32 3x3/s1/p1 same-size weight gradient (pu_wgrad_tile's
-    loader kind: 1 float4 GEMM, 2 small-channel direct, 3 halo, 4 stem, 5 Winograd-domain)."""
-    a = WgradArgs(batch, hw[0], hw[1], hw[0], hw[1], 3, 3, 1, 1, 16, n, 16, c0, 16 if c1 else None, c1, 1, 16, 16,
+def wgrad_kind(*, batch, hw, n, c0, c1=0, k=3):
+    """Which kernel pu_wgrad takes for an fp32 kxk/s1 same-size ('same' padding) weight gradient
+    (pu_wgrad_tile's loader kind: 1 float4 GEMM, 2 small-channel direct, 3 halo, 4 stem,
+    5 Winograd-domain, 6 pointwise)."""
+    a = WgradArgs(batch, hw[0], hw[1], hw[0], hw[1], k, k, 1, (k - 1) // 2, 16, n, 16, c0, 16 if c1 else None, c1, 1,
+                  16, 16,
                   0, 1 if _FP32_MATH == "split6" else 0)
     bn, bk, qv, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     check(lib().pu_wgrad_tile(ctypes.byref(a), ctypes.byref(bn), ctypes.byref(bk), ctypes.byref(qv), ctypes.byref(sp)),

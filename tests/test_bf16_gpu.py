@@ -212,6 +212,46 @@ def test_bf16_halo_conv_bit_identical_to_lean(c0, cout):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("B,H,epi", [(2, 128, "relu"), (3, 128, "mask"), (1, 128, "resid"), (2, 128, "accum"),
+                                     (1, 128, "plain")])
+def test_bf16_rows_conv_bit_identical_to_lean(B, H, epi):
+    """the row-stream kernel (128-wide 64 -> 64 3x3: weights resident in LDS, 16-row strips) sums
+    the same bf16 products in the same order as the per-tap lean kernel: bit-identical outputs with
+    every epilogue option (bias + ReLU, mask, residual, accumulate)"""
+    from punet._lib import PU_PACK_CONV_FWD
+    g = torch.Generator(device=DEV).manual_seed(H + B + len(epi))
+    x = torch.randn(B, H, 128, 64, device=DEV, generator=g).to(BF)
+    w = torch.randn(64, 64, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(64, device=DEV, generator=g)
+    aux = torch.randn(B, H, 128, 64, device=DEV, generator=g).to(BF)
+    outs = []
+    prev = K.set_conv_halo(1)
+    try:
+        for halo in (1, 0):               # row-stream (the default route for this shape) vs per-tap
+            K.set_conv_halo(halo)
+            pk = T._Packs()
+            wt = pk.get(w, PU_PACK_CONV_FWD, 576, 32, BF)
+            out = aux.clone() if epi == "accum" else torch.empty_like(x)
+            K.igemm(batch=B, in_hw=(H, 128), out_hw=(H, 128), k=3, stride=1, pad=1, src0=x, c0=64, weight=wt,
+                    k_pad=576, n=64, dst0=out, bias=None if epi == "plain" else b, relu=epi == "relu",
+                    mask0=aux if epi == "mask" else None, resid=aux if epi == "resid" else None,
+                    accum=epi == "accum", cgroup=32)
+            outs.append(out)
+    finally:
+        K.set_conv_halo(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.to(BF).float(), None if epi == "plain" else b,
+                                     padding=1).permute(0, 2, 3, 1)
+    if epi == "relu":
+        ref = ref.relu()
+    elif epi == "mask":
+        ref = torch.where(aux.float() > 0, ref, torch.zeros_like(ref))
+    elif epi in ("resid", "accum"):
+        ref = ref + aux.float()
+    assert torch.allclose(outs[0].float(), ref, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("B,H,c0,c1,cout", [(8, 128, 64, 0, 64), (4, 128, 32, 32, 128), (8, 64, 128, 0, 64),
                                             (16, 32, 64, 64, 192), (3, 32, 96, 0, 64)])
 def test_bf16_halo2_conv_matches_fp32_and_halo1(B, H, c0, c1, cout):

@@ -137,6 +137,34 @@ def test_small_channel_wgrad_without_bias(C, N):
     assert_close(dw0, ref)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,N,bias", [(4, 8, True), (4, 8, False), (3, 8, True), (4, 16, True), (3, 4, False)])
+def test_pointwise_wgrad(C, N, bias):
+    """The 1x1 small-channel weight gradient (wgrad_pw_kernel, C4's CoordConv conv): against the fp64
+    torch gradient, bias_mode 0 equal to bias_mode 1's weights, bitwise run to run."""
+    assert K.wgrad_kind(batch=3, hw=(40, 56), n=N, c0=C, k=1) == 6
+    g = torch.Generator().manual_seed(C * 100 + N)
+    B, H, W = 3, 40, 56
+    x = nhwc(rnd(B, C, H, W, g=g)).to(DEV)
+    dz = nhwc(rnd(B, N, H, W, g=g)).to(DEV)
+
+    def run():
+        dw = torch.full((N, C, 1, 1), float("nan"), device=DEV)
+        db = torch.full((N,), float("nan"), device=DEV) if bias else None
+        K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, rows=dz, n=N, src0=x, c0=C,
+                dweight=dw, bias_mode=1 if bias else 0, dbias=db)
+        return dw, db
+
+    dw, db = run()
+    dw2, db2 = run()
+    assert torch.equal(dw, dw2) and (not bias or torch.equal(db, db2))
+    xr, gr = nchw(x).cpu().double(), nchw(dz).cpu().double()
+    ref = torch.einsum("bchw,bnhw->nc", xr, gr).reshape(N, C, 1, 1)
+    assert torch.allclose(dw.cpu().double(), ref, rtol=1e-5, atol=1e-4), (dw.cpu().double() - ref).abs().max()
+    if bias:
+        assert torch.allclose(db.cpu().double(), gr.sum((0, 2, 3)), rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("B,H,W,c0,c1,cout", SMALL_X6_CASES)
 def test_conv3x3_small_channel_x6(B, H, W, c0, c1, cout):
     prev = K.set_smallx6(True)
