@@ -1229,6 +1229,16 @@ static bool lean_ok_b(const pu_conv_args* a) {
 
 // lean tiles: 256 x 128 (N > 64) or 256 x 64, 4 waves, ~2 resident blocks per CU (72 / 61 KB of
 // LDS); small pixel grids split K on group boundaries until ~2 blocks per CU
+// PU_BF16_LEAN128=1: 128 x 128 tiles instead of a K split when they alone give a round of blocks
+// (C3's 16^2 level: 256 tiles; the split's fp32 partials cost 2 x 67 MB per layer there)
+static bool lean128_on() {
+    static const bool on = [] {
+        const char* e = getenv("PU_BF16_LEAN128");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 static void plan_lean_b(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
     *bm = 256;
     *bn = a->n > 64 ? 128 : 64;
@@ -1238,6 +1248,10 @@ static void plan_lean_b(const pu_conv_args* a, long long M, int* bm, int* bn, in
     const int tiles = blocks_for_b(M, a->n, *bm, *bn);
     const int target = 512;
     if (tiles >= target - target / 16) return;
+    if (lean128_on() && a->n > 64 && blocks_for_b(M, a->n, 128, 128) >= 240) {
+        *bm = 128;
+        return;
+    }
     int ks = ceil_div(target, tiles);
     if (ks > T / 9) ks = T / 9;
     if (ks < 2) return;
@@ -1366,7 +1380,8 @@ extern "C" int pu_conv_igemm_bf16(const pu_conv_args* a, void* stream) {
     }
     p.part = (float*)a->workspace;
     const dim3 grid(ceil_div(M, bm) * p.gn * p.ksplit);
-    if (lean && bn == 128) hipLaunchKernelGGL((igemm_bf16_lean_kernel<256, 128, 2, 2, 4>), grid, dim3(256), 0, s, p);
+    if (lean && bm == 128) hipLaunchKernelGGL((igemm_bf16_lean_kernel<128, 128, 2, 2, 4>), grid, dim3(256), 0, s, p);
+    else if (lean && bn == 128) hipLaunchKernelGGL((igemm_bf16_lean_kernel<256, 128, 2, 2, 4>), grid, dim3(256), 0, s, p);
     else if (lean) hipLaunchKernelGGL((igemm_bf16_lean_kernel<256, 64, 4, 1, 4>), grid, dim3(256), 0, s, p);
     else if (bm == 256) hipLaunchKernelGGL((igemm_bf16_kernel<256, 64, 4, 1, 3>), grid, dim3(256), 0, s, p);
     else if (bm == 128 && bn == 128) hipLaunchKernelGGL((igemm_bf16_kernel<128, 128, 2, 2, 3>), grid, dim3(256), 0, s, p);

@@ -88,6 +88,11 @@ def test_channel_scale_and_column_sum():
     m = (torch.rand(3, 12, generator=g) > 0.5).float() * 2.0
     y = K.channel_scale(x.to(DEV), m.to(DEV))
     assert torch.equal(y.cpu(), x * m[:, None, None, :])
+    xb = rnd(5, 64, 48, 8, g=g).to(DEV)            # in place, several grid rows per image
+    mb = torch.rand(5, 8, generator=g)
+    ref = xb.cpu() * mb[:, None, None, :]
+    K.channel_scale(xb, mb.to(DEV), out=xb)
+    assert torch.equal(xb.cpu(), ref)
     xs = rnd(3, 5, 7, 6, g=g)                       # odd channel count: scalar path
     ms = torch.rand(3, 6, generator=g)
     assert torch.equal(K.channel_scale(xs.to(DEV), ms.to(DEV)).cpu(), xs * ms[:, None, None, :])
