@@ -19,7 +19,27 @@ import re
 import sys
 
 
-def tag_of(name):
+def tag_of(name, grid=None):
+    # the Winograd kernels: bench.py tags unsplit launches igemm<256x64,wino> (grid 256 x 512
+    # threads, persistent or one block per item) and split-K ones with ",k<n>" (fewer items)
+    if "wgrad_wino_x6_kernel" in name:
+        return "wgrad<64x576,wino,x6>"
+    if "wino_x6_kernel" in name:
+        return "igemm<256x64,wino>" if grid is None or int(grid) >= 131072 else "igemm<256x64,wino,split>"
+    if "igemm_bf16_rows_kernel" in name:
+        return "igemm_bf16<128x64,rows>"
+    m = re.search(r"igemm_bf16_halo_kernel<(\d+)>", name)
+    if m:
+        return "igemm_bf16<256x64,halo>"
+    m = re.search(r"igemm_bf16_halo2_kernel<(\d+)>", name)
+    if m:
+        return "igemm_bf16<512x64,halo>"
+    m = re.search(r"igemm_bf16_lean_kernel<(\d+), (\d+),", name)
+    if m:
+        return "igemm_bf16<%sx%s,lean>" % m.groups()
+    m = re.search(r"wgrad_halo_bf16_kernel<(\d)>", name)
+    if m:
+        return "wgrad_bf16<%dx576,halo>" % (64 * int(m.group(1)))
     if "wgrad_halo_x6_kernel<2>" in name:
         return "wgrad<128x576,halo,x6>"
     if "wgrad_halo_x6_kernel" in name:
@@ -58,13 +78,14 @@ def load(d):
         for r in csv.DictReader(open(f)):
             key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), r["Counter_Name"])
             per[key] += float(r["Counter_Value"])      # summed over dimensions (XCD/SE instances)
-            names[key[0]] = r.get("Kernel_Name", "?")
+            names[key[0]] = (r.get("Kernel_Name", "?"), r.get("Grid_Size"))
         for (disp, cn), v in per.items():
-            vals[tag_of(names[disp])][cn].append(v)
+            vals[tag_of(*names[disp])][cn].append(v)
     durs = collections.defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            durs[tag_of(r["Kernel_Name"])].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+            grid = r.get("Grid_Size") or r.get("Grid_Size_X")
+            durs[tag_of(r["Kernel_Name"], grid)].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     return vals, durs
 
 

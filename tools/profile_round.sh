@@ -37,6 +37,15 @@ tail -1 $OUT/c3.log > $OUT/c3.json
 step "c3 kernel-trace stats"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c3_stats -o run -- \
     $B --config c3 --no-cpu-baseline --no-oja > $OUT/c3_stats.log 2>&1 || { tail -20 $OUT/c3_stats.log; exit 1; }
+for pass in "fetch FETCH_SIZE" "write WRITE_SIZE" "clock GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES"; do
+  set -- $pass
+  name=$1; shift
+  step "c3 pmc $name ($*)"
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $OUT/c3pmc/$name -o run -- \
+      $B --config c3 --no-cpu-baseline --no-oja --no-kernel-profile --steps 3 --warmup 1 > $OUT/c3pmc_$name.log 2>&1 \
+      || { tail -20 $OUT/c3pmc_$name.log; exit 1; }
+done
+python tools/pmc_traffic.py $OUT/c3pmc $OUT/c3_pmc_traffic.json > $OUT/c3_pmc_traffic.txt 2>&1 || { cat $OUT/c3_pmc_traffic.txt; exit 1; }
 step "c4 bench"
 timeout -k 10 300 $B --config c4 > $OUT/c4.log 2>&1 || { tail -20 $OUT/c4.log; exit 1; }
 tail -1 $OUT/c4.log > $OUT/c4.json
