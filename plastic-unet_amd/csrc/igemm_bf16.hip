@@ -959,6 +959,12 @@ __global__ __launch_bounds__(H2_NT) void igemm_bf16_halo2_kernel(const IgemmBf16
 //     start of its step (they land under its MFMAs), 8-byte stores.
 // K order (32-channel group, tap, 16-channel half) and the MFMA sequence per accumulator are
 // igemm_bf16_halo_kernel's, so the two are bit-identical.  Host: rows_ok_b.
+#ifndef PU_RS_PD
+#define PU_RS_PD 4      // k-steps of fragment reads in flight (A/B builds: 2, 3, 4)
+#endif
+#ifndef PU_RS_ABL
+#define PU_RS_ABL 0     // ablation builds only (timing): 1 no output stores, 2 no MFMAs, 3 no per-row wait/barrier
+#endif
 constexpr int RS_W = 128, RS_ROWS = 16, RS_RING = 5;
 constexpr int RS_ROWB = (RS_W + 2) * 128;                        // 16640 B per ring row
 constexpr int RS_WB = 9 * 64 * 128;                              // 73728 B of weights
@@ -1038,9 +1044,10 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
     for (int r = r0; r < r0 + RS_ROWS; ++r) {
         // input row r+1 landed (issued two steps ago; later: stores, the epilogue loads and one row)
         if (r == r0) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");   // + the padding zeros
+        else if (PU_RS_ABL == 3) asm volatile("" ::: "memory");
         else if (r == r0 + 1) wait_vm_plus<12>(E);
         else wait_vm_plus<20>(E);
-        __builtin_amdgcn_s_barrier();                             // ... for every wave; slot of row r-2 free
+        if (PU_RS_ABL != 3 || r == r0) __builtin_amdgcn_s_barrier();   // ... for every wave; slot of row r-2 free
         asm volatile("" ::: "memory");
         const long long m = (long long)(b * p.Ho + r) * RS_W + q0 + lr;
         bf16x4 mv[2][4], rv[2][4], av[2][4];
@@ -1063,23 +1070,29 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
-        bf16x8 fx[3], fw[3][2];
+        // fragment reads RS_PD k-steps ahead (3 x 16 B per step; 12 in flight at RS_PD = 4 - one wave
+        // per SIMD has no partner wave to cover the LDS latency: at 2 steps ahead the loop ran at the
+        // read latency, 3.4 us per row with or without its MFMAs)
+        constexpr int RS_PD = PU_RS_PD, NB = RS_PD + 1;
+        bf16x8 fx[NB], fw[NB][2];
         auto rd = [&](auto S) {
             constexpr int s = decltype(S)::value;
             constexpr int g = s / 18, t = (s % 18) / 2, kk = s % 2, u = g * 2 + kk;
-            fx[s % 3] = *reinterpret_cast<const bf16x8*>(rs_lds + sb[t / 3] + xoff[t % 3][u]);
+            fx[s % NB] = *reinterpret_cast<const bf16x8*>(rs_lds + sb[t / 3] + xoff[t % 3][u]);
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                fw[s % 3][j] = *reinterpret_cast<const bf16x8*>(wl + (t * 64 + j * 32) * 128 + woff[u]);
+                fw[s % NB][j] = *reinterpret_cast<const bf16x8*>(wl + (t * 64 + j * 32) * 128 + woff[u]);
         };
-        rd(std::integral_constant<int, 0>{});
-        rd(std::integral_constant<int, 1>{});
+        static_for<RS_PD>([&](auto S) { rd(S); });
         static_for<36>([&](auto S) {
             constexpr int s = decltype(S)::value;
-            if constexpr (s + 2 < 36) rd(std::integral_constant<int, s + 2>{});
+            if constexpr (s + RS_PD < 36) rd(std::integral_constant<int, s + RS_PD>{});
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[s % 3][j], fx[s % 3], acc[j], 0, 0, 0);
+            for (int j = 0; j < 2; ++j) {
+                if (PU_RS_ABL == 2) acc[j][s & 15] += __builtin_bit_cast(float, __builtin_shufflevector(fw[s % NB][j], fx[s % NB], 0, 9));
+                else acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[s % NB][j], fx[s % NB], acc[j], 0, 0, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
         });
 
@@ -1111,7 +1124,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
                 bf16x4 o;
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
-                *reinterpret_cast<bf16x4*>(p.dst0 + m * 64 + j * 32 + 8 * q + 4 * lh) = o;
+                if (PU_RS_ABL != 1 || (p.flags & (1 << 30))) *reinterpret_cast<bf16x4*>(p.dst0 + m * 64 + j * 32 + 8 * q + 4 * lh) = o;
             }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // the trailing (empty) row loads drain
@@ -1229,12 +1242,13 @@ static bool lean_ok_b(const pu_conv_args* a) {
 
 // lean tiles: 256 x 128 (N > 64) or 256 x 64, 4 waves, ~2 resident blocks per CU (72 / 61 KB of
 // LDS); small pixel grids split K on group boundaries until ~2 blocks per CU
-// PU_BF16_LEAN128=1: 128 x 128 tiles instead of a K split when they alone give a round of blocks
-// (C3's 16^2 level: 256 tiles; the split's fp32 partials cost 2 x 67 MB per layer there)
+// 128 x 128 tiles instead of a K split when they alone give a round of blocks (C3's 16^2 level:
+// 256 tiles; the split's fp32 partials cost 2 x 67 MB per layer there): l4 fwd / dgrad 65 / 70 ->
+// 56 / 56 us, C3 +0.8 %; PU_BF16_LEAN128=0 keeps the split (A/B runs)
 static bool lean128_on() {
     static const bool on = [] {
         const char* e = getenv("PU_BF16_LEAN128");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     return on;
 }
