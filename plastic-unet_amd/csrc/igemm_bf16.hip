@@ -963,7 +963,8 @@ __global__ __launch_bounds__(H2_NT) void igemm_bf16_halo2_kernel(const IgemmBf16
 #define PU_RS_PD 4      // k-steps of fragment reads in flight (A/B builds: 2, 3, 4)
 #endif
 #ifndef PU_RS_ABL
-#define PU_RS_ABL 0     // ablation builds only (timing): 1 no output stores, 2 no MFMAs, 3 no per-row wait/barrier
+#define PU_RS_ABL 0     // ablation builds only (timing): 1 no output stores, 2 no MFMAs, 3 no per-row wait/barrier,
+// 4 in-loop row loads with an empty range (no HBM reads), 5 weights with an empty range
 #endif
 constexpr int RS_W = 128, RS_ROWS = 16, RS_RING = 5;
 constexpr int RS_ROWB = (RS_W + 2) * 128;                        // 16640 B per ring row
@@ -996,7 +997,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
         const int tap = row >> 6, n = row & 63;
         const int c = (lane & 7) ^ ((row >> 1) & 7);
         const unsigned vo = (unsigned)(n * p.k_pad + (c >> 2) * 288 + tap * 32 + (c & 3) * 8) * 2u;
-        lean_load(p.wt, wbytes, wl + I * 1024, vo, 0u);
+        lean_load(p.wt, PU_RS_ABL == 5 ? 0u : wbytes, wl + I * 1024, vo, 0u);
     }
     // input row ir of image b -> ring slot (ir + 1) % RS_RING, pixels 1 .. 128 (4 x 1 KB per wave)
     unsigned xvo[4];
@@ -1012,7 +1013,8 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
         char* base = rs_lds + ((ir + 1) % RS_RING) * RS_ROWB + 128;
         const unsigned soff = ok ? (unsigned)((b * p.Hi + ir) * RS_W) * 128u : 0u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) lean_load(p.src0, ok ? xbytes : 0u, base + (wave + 4 * j) * 1024, xvo[j], soff);
+        for (int j = 0; j < 4; ++j)
+            lean_load(p.src0, ok && !(PU_RS_ABL == 4 && ir > r0 + 2) ? xbytes : 0u, base + (wave + 4 * j) * 1024, xvo[j], soff);
     };
     load_row(r0 - 1);
     load_row(r0);
@@ -1040,28 +1042,35 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
             bias4[j][q] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + j * 32 + 8 * q + 4 * lh) : f32x4{0.f, 0.f, 0.f, 0.f};
     const bool has_m = p.mask0 != nullptr, has_r = p.resid != nullptr, has_a = (p.flags & PU_EPI_ACCUM) != 0;
     const int E = 8 * ((has_m ? 1 : 0) + (has_r ? 1 : 0) + (has_a ? 1 : 0));
+    // epilogue operands of row rr, loaded after the previous row's stores: they land during row
+    // rr's MFMAs, and waiting for them does not wait for the row loads issued later
+    bf16x4 mv[2][4], rv[2][4], av[2][4];
+    auto prefetch = [&](int rr) {
+        const long long mm = (long long)(b * p.Ho + rr) * RS_W + q0 + lr;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const long long off = mm * 64 + j * 32 + 8 * q + 4 * lh;
+                if (has_m) mv[j][q] = *reinterpret_cast<const bf16x4*>(p.mask0 + off);
+                if (has_r) rv[j][q] = *reinterpret_cast<const bf16x4*>(p.resid + off);
+                if (has_a) av[j][q] = *reinterpret_cast<const bf16x4*>(p.dst0 + off);
+            }
+    };
+    if (E) prefetch(r0);
 
     for (int r = r0; r < r0 + RS_ROWS; ++r) {
-        // input row r+1 landed (issued two steps ago; later: stores, the epilogue loads and one row)
-        if (r == r0) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");   // + the padding zeros
-        else if (PU_RS_ABL == 3) asm volatile("" ::: "memory");
-        else if (r == r0 + 1) wait_vm_plus<12>(E);
-        else wait_vm_plus<20>(E);
+        // input row r+1 landed (issued two steps ago; issued after it: stores (8), epilogue loads (E),
+        // one row (4), stores, epilogue loads - over-waiting where the count is not exact)
+        if (r == r0) {
+            wait_vm_plus<4>(E);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // + the padding zeros
+        } else if (PU_RS_ABL == 3) asm volatile("" ::: "memory");
+        else if (r == r0 + 1) wait_vm_plus<12>(2 * E);
+        else wait_vm_plus<20>(2 * E);
         if (PU_RS_ABL != 3 || r == r0) __builtin_amdgcn_s_barrier();   // ... for every wave; slot of row r-2 free
         asm volatile("" ::: "memory");
         const long long m = (long long)(b * p.Ho + r) * RS_W + q0 + lr;
-        bf16x4 mv[2][4], rv[2][4], av[2][4];
-        if (E) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const long long off = m * 64 + j * 32 + 8 * q + 4 * lh;
-                    if (has_m) mv[j][q] = *reinterpret_cast<const bf16x4*>(p.mask0 + off);
-                    if (has_r) rv[j][q] = *reinterpret_cast<const bf16x4*>(p.resid + off);
-                    if (has_a) av[j][q] = *reinterpret_cast<const bf16x4*>(p.dst0 + off);
-                }
-        }
         load_row(r + 3);
 
         const int sb[3] = {(r % RS_RING) * RS_ROWB, ((r + 1) % RS_RING) * RS_ROWB, ((r + 2) % RS_RING) * RS_ROWB};
@@ -1096,7 +1105,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
             __builtin_amdgcn_sched_barrier(0);
         });
 
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");         // this row's epilogue operands
+        if (E) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this row's epilogue operands
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -1126,6 +1135,7 @@ __global__ __launch_bounds__(256) void igemm_bf16_rows_kernel(const IgemmBf16Par
                 for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
                 if (PU_RS_ABL != 1 || (p.flags & (1 << 30))) *reinterpret_cast<bf16x4*>(p.dst0 + m * 64 + j * 32 + 8 * q + 4 * lh) = o;
             }
+        if (E && r + 1 < r0 + RS_ROWS) prefetch(r + 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // the trailing (empty) row loads drain
 }
