@@ -1,6 +1,6 @@
 #!/bin/bash
 # kernel traces of short bench runs (per (kernel, grid) averages) for the given configs
-#   bash tools/c2_trace.sh <tag> [configs...]
+#   bash tools/kernel_trace.sh <tag> [configs...]
 set -u
 OUT=gpurun_out/${1:-ktrace}; shift
 CFGS=${@:-c2 c3}
