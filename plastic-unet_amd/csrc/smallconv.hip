@@ -20,19 +20,31 @@
 
 namespace pu {
 
-constexpr int SX_TH = 16, SX_TW = 32;                 // output tile
-constexpr int SX_HH = SX_TH + 2, SX_HW = SX_TW + 2;   // halo
-constexpr int SX_HP = SX_HH * SX_HW;                  // halo pixels (612)
+constexpr int SX_TW = 32, SX_HW = SX_TW + 2;         // output tile width, halo width
+// output tile height: 16 rows for C = 8 (29 KB of split halo images, 5 blocks per CU); 8 rows for
+// C = 16, whose 16-row images (59 KB) held the kernel to 2 blocks per CU - at 33 KB it runs 4
+// (PU_SX16_TH=16 restores the 16-row tile for A/B runs)
+#ifndef PU_SX16_TH
+#define PU_SX16_TH 8
+#endif
+template <int C> constexpr int sx_th() { return C == 8 ? 16 : PU_SX16_TH; }
+template <int C> constexpr int sx_hp() { return (sx_th<C>() + 2) * SX_HW; }   // halo pixels (612 / 340)
 
 typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
 typedef float f32x4s __attribute__((ext_vector_type(4)));
 
-// LDS allows 4-5 / 2 blocks per CU (29 / 59 KB): waves_per_eu(4 / 2) lets the compiler use 128 / 256
-// registers instead of squeezing into 64 with the accumulators parked in AGPRs (320 accvgpr moves
-// per wave at C = 8)
+// LDS allows 4-5 blocks per CU (29 / 33 KB): waves_per_eu(4) lets the compiler use 128 registers
+// instead of squeezing into 64 with the accumulators parked in AGPRs (320 accvgpr moves per wave at
+// C = 8)
+// One block per tile.  LDS allows 4-5 blocks per CU (29 / 33 KB): waves_per_eu(4) lets the compiler
+// use 128 registers instead of squeezing into 64 with the accumulators parked in AGPRs (320 accvgpr
+// moves per wave at C = 8)
 template <int C, int N>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 8 ? 4 : 2))) void smallconv_x6_kernel(const IgemmParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() == 16 && C == 16 ? 2 : 4))) void smallconv_x6_kernel(const IgemmParams p) {
 #pragma clang fp contract(off)
+    constexpr int SX_TH = sx_th<C>(), SX_HP = sx_hp<C>();
+    constexpr int RPW = SX_TH / 4;                  // output rows per wave
+    constexpr int GR = 2 * RPW;                     // 16-pixel groups per wave
     constexpr int HALVES = C / 8;                   // 8-channel LDS images per plane
     constexpr int KS = (9 * C + 31) / 32;           // 32-wide k steps
     // [plane][half][pixel][8 channels] bf16
@@ -111,11 +123,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 8 ? 4 
     }
     __syncthreads();
 
-    // ---- MFMAs: wave w owns output rows 4w .. 4w+3, each 2 groups of 16 pixels (8 groups)
+    // ---- MFMAs: wave w owns output rows RPW w .. RPW w + RPW-1, each 2 groups of 16 pixels
     const int j = lane & 15, g = lane >> 4;
-    f32x4s acc[8];
+    f32x4s acc[GR];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] = f32x4s{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < GR; ++t) acc[t] = f32x4s{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
         const int k = 32 * s + 8 * g;               // this lane's 8 k: one tap, 8 channels
@@ -123,8 +135,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 8 ? 4 
         const bool live = tap < 9;
         const int r = live ? tap / 3 : 0, sx = live ? tap % 3 : 0;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int row = 4 * wave + (t >> 1), col = (t & 1) * 16 + j;
+        for (int t = 0; t < GR; ++t) {
+            const int row = RPW * wave + (t >> 1), col = (t & 1) * 16 + j;
             const int hp = (row + r) * SX_HW + col + sx;
             // k past 9C (tap >= 9) reads tap 0's window: finite values against zero weight planes
             bf16x8s xb[3];
@@ -145,8 +157,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 8 ? 4 
     // ---- epilogue: lane holds channels 4g .. 4g+3 of pixel (row, col)
     if (4 * g >= N) return;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        const int oy = tyi * SX_TH + 4 * wave + (t >> 1), ox = txi * SX_TW + (t & 1) * 16 + j;
+    for (int t = 0; t < GR; ++t) {
+        const int oy = tyi * SX_TH + RPW * wave + (t >> 1), ox = txi * SX_TW + (t & 1) * 16 + j;
         if (oy >= p.Ho || ox >= p.Wo) continue;
         const int m = (b * p.Ho + oy) * p.Wo + ox;
         epi_store4(p, epi_row(p, m), 4 * g, acc[t]);
@@ -165,7 +177,8 @@ bool smallx6_ok(const pu_conv_args* a, bool vec_epi) {
 
 int smallx6_launch(const pu_conv_args* a, const IgemmParams& p, hipStream_t s) {
     const int C = a->c0 + a->c1;
-    const dim3 grid((unsigned)(((a->out_w + SX_TW - 1) / SX_TW) * ((a->out_h + SX_TH - 1) / SX_TH) * a->batch));
+    const int th = C == 8 ? sx_th<8>() : sx_th<16>();
+    const dim3 grid((unsigned)(((a->out_w + SX_TW - 1) / SX_TW) * ((a->out_h + th - 1) / th) * a->batch));
     if (C == 8 && a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 8>), grid, dim3(256), 0, s, p);
     else if (C == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 16>), grid, dim3(256), 0, s, p);
     else if (a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<16, 8>), grid, dim3(256), 0, s, p);
