@@ -34,8 +34,8 @@ def eval_net(net, X_val, y_val, device, criterion=None, debug=False, batch=32):
             losses = torch.stack([criterion(yf[b], tf[b]) if criterion is not None else bce_loss(yf[b], tf[b])
                                   for b in range(B)])
             # one device->host copy per chunk; the per-sample sums in the reference's order
-            for b, l in enumerate(losses.cpu().tolist()):
-                total_loss += l
+            for sample_loss in losses.cpu().tolist():
+                total_loss += sample_loss
             y_np, t_np = yf.cpu().numpy(), tf.cpu().numpy()
             for b in range(B):
                 total_acc += fast_iou_metric(y_true_in=t_np[b], y_pred_in=y_np[b])
