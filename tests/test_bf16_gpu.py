@@ -253,6 +253,29 @@ def test_bf16_rows_conv_bit_identical_to_lean(B, H, epi):
     assert torch.allclose(outs[0].float(), ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("B,H", [(3, 16), (1, 48), (2, 112)])
+def test_bf16_rows_conv_strip_edges(B, H):
+    """the row-stream kernel on grids of 1, 3 and 7 16-row strips (first / last strip padding rows,
+    a strip that is both): fwd (bias + ReLU) and dgrad (mask) within the bf16 bound of torch fp32 on
+    the bf16-rounded operands"""
+    g = torch.Generator(device=DEV).manual_seed(B * 1000 + H)
+    x = torch.randn(B, H, 128, 64, device=DEV, generator=g).relu().to(BF)
+    w = torch.randn(64, 64, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(64, device=DEV, generator=g)
+    dz = torch.randn(B, H, 128, 64, device=DEV, generator=g).to(BF)
+    pk = T._Packs()
+    y = T.conv3x3(x, w, b, pk)
+    d0, _ = T.conv3x3_dgrad(dz, w, pk, mask0=x)
+    torch.cuda.synchronize()
+    wb = w.to(BF).float()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wb, b, padding=1).relu().permute(0, 2, 3, 1)
+    refd = F.conv_transpose2d(dz.float().permute(0, 3, 1, 2), wb, padding=1).permute(0, 2, 3, 1)
+    refd = torch.where(x.float() > 0, refd, torch.zeros_like(refd))
+    for out, r in ((y, ref), (d0, refd)):
+        err = (out.float() - r).abs().max().item()
+        assert err <= 2e-2 * r.abs().max().item() + 1e-3, err
+
+
 @pytest.mark.parametrize("B,H,c0,c1,cout", [(8, 128, 64, 0, 64), (4, 128, 32, 32, 128), (8, 64, 128, 0, 64),
                                             (16, 32, 64, 64, 192), (3, 32, 96, 0, 64)])
 def test_bf16_halo2_conv_matches_fp32_and_halo1(B, H, c0, c1, cout):
