@@ -16,6 +16,14 @@
 //   D (16 x 16, 4 registers): lane holds 4 consecutive channels of one pixel -> igemm's float4
 //       epilogue (bias, residual, ReLU, masks, concat split, accumulate).
 // Each wave owns 4 output rows x 32 pixels = 8 groups of 16 pixels: 8 accumulators of 4 registers.
+//
+// Row pairs (N = 8, the default; PU_SX_PAIR=0 disables): with 8 output channels rows 8..15 of A
+// were zero - half of every MFMA wasted - and K = 9C was padded to a multiple of 32.  Instead a
+// group covers TWO output rows y, y+1 of 16 pixels: k runs over 12 "super-taps" (input rows
+// y-1 .. y+2 x 3 columns) x C channels (96 / 192 = exactly 3 / 6 k-steps), A row n < 8 holds
+// W[n][dy][dx] for super-tap (dy, dx) (zero for dy = 3), row 8 + n holds W[n][dy-1][dx] (zero
+// for dy = 0), so D rows 0..7 are output row y and rows 8..15 output row y+1: the MFMAs per
+// output pixel halve (C = 8) or drop 40 % (C = 16), and every lane stores in the epilogue.
 #include "conv_common.h"
 
 namespace pu {
@@ -26,6 +34,9 @@ constexpr int SX_TW = 32, SX_HW = SX_TW + 2;         // output tile width, halo 
 // (PU_SX16_TH=16 restores the 16-row tile for A/B runs)
 #ifndef PU_SX16_TH
 #define PU_SX16_TH 8
+#endif
+#ifndef PU_SX_PAIR
+#define PU_SX_PAIR 1
 #endif
 template <int C> constexpr int sx_th() { return C == 8 ? 16 : PU_SX16_TH; }
 template <int C> constexpr int sx_hp() { return (sx_th<C>() + 2) * SX_HW; }   // halo pixels (612 / 340)
@@ -43,10 +54,12 @@ template <int C, int N>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() == 16 && C == 16 ? 2 : 4))) void smallconv_x6_kernel(const IgemmParams p) {
 #pragma clang fp contract(off)
     constexpr int SX_TH = sx_th<C>(), SX_HP = sx_hp<C>();
+    constexpr bool PAIR = PU_SX_PAIR && N == 8;     // two output rows per group (header)
     constexpr int RPW = SX_TH / 4;                  // output rows per wave
-    constexpr int GR = 2 * RPW;                     // 16-pixel groups per wave
+    constexpr int GR = PAIR ? RPW : 2 * RPW;        // groups (16 pixels x 1 or 2 rows) per wave
     constexpr int HALVES = C / 8;                   // 8-channel LDS images per plane
-    constexpr int KS = (9 * C + 31) / 32;           // 32-wide k steps
+    constexpr int KS = PAIR ? 12 * C / 32 : (9 * C + 31) / 32;   // 32-wide k steps
+    static_assert(!PAIR || RPW % 2 == 0, "row pairs need an even number of rows per wave");
     // [plane][half][pixel][8 channels] bf16
     __shared__ __attribute__((aligned(16))) __bf16 img[3 * HALVES * SX_HP * 8];
 
@@ -71,7 +84,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
         for (int s = 0; s < KS; ++s) {
             f32x4s lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
             const int k = 32 * s + 8 * g;
-            if (n < N && k < 9 * C) {      // 9C is a multiple of 8: the 8 k are all real or all padding
+            if (PAIR) {                    // super-tap (dy, dx) of output row y + (n >> 3)
+                const int st = k / C, dy = st / 3 - (n >> 3), wk = (dy * 3 + st % 3) * C + k % C;
+                if (dy >= 0 && dy <= 2) {
+                    lo = *reinterpret_cast<const f32x4s*>(p.wt + (n & 7) * p.k_pad + wk);
+                    hi = *reinterpret_cast<const f32x4s*>(p.wt + (n & 7) * p.k_pad + wk + 4);
+                }
+            } else if (n < N && k < 9 * C) {   // 9C is a multiple of 8: the 8 k are all real or all padding
                 lo = *reinterpret_cast<const f32x4s*>(p.wt + n * p.k_pad + k);
                 hi = *reinterpret_cast<const f32x4s*>(p.wt + n * p.k_pad + k + 4);
             }
@@ -130,13 +149,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
     for (int t = 0; t < GR; ++t) acc[t] = f32x4s{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-        const int k = 32 * s + 8 * g;               // this lane's 8 k: one tap, 8 channels
+        const int k = 32 * s + 8 * g;               // this lane's 8 k: one (super-)tap, 8 channels
         const int tap = k / C, c8 = (k % C) / 8;
-        const bool live = tap < 9;
+        const bool live = PAIR || tap < 9;
         const int r = live ? tap / 3 : 0, sx = live ? tap % 3 : 0;
 #pragma unroll
         for (int t = 0; t < GR; ++t) {
-            const int row = RPW * wave + (t >> 1), col = (t & 1) * 16 + j;
+            const int row = RPW * wave + (PAIR ? 2 * (t >> 1) : t >> 1), col = (t & 1) * 16 + j;
             const int hp = (row + r) * SX_HW + col + sx;
             // k past 9C (tap >= 9) reads tap 0's window: finite values against zero weight planes
             bf16x8s xb[3];
@@ -154,14 +173,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
         }
     }
 
-    // ---- epilogue: lane holds channels 4g .. 4g+3 of pixel (row, col)
-    if (4 * g >= N) return;
+    // ---- epilogue: lane holds channels 4g .. 4g+3 of pixel (row, col); row pairs: channels
+    // 4 (g & 1) .. +3 of row + (g >> 1)
+    if (!PAIR && 4 * g >= N) return;
 #pragma unroll
     for (int t = 0; t < GR; ++t) {
-        const int oy = tyi * SX_TH + RPW * wave + (t >> 1), ox = txi * SX_TW + (t & 1) * 16 + j;
+        const int oy = tyi * SX_TH + RPW * wave + (PAIR ? 2 * (t >> 1) + (g >> 1) : t >> 1);
+        const int ox = txi * SX_TW + (t & 1) * 16 + j;
         if (oy >= p.Ho || ox >= p.Wo) continue;
         const int m = (b * p.Ho + oy) * p.Wo + ox;
-        epi_store4(p, epi_row(p, m), 4 * g, acc[t]);
+        epi_store4(p, epi_row(p, m), PAIR ? 4 * (g & 1) : 4 * g, acc[t]);
     }
 }
 

@@ -77,6 +77,9 @@ SMALL_X6_CASES = [
     (2, 64, 64, 16, 0, 8),      # 16 -> 8 (dgrad 8 -> 16)
     (1, 17, 36, 16, 0, 16),     # 16 -> 16, odd height
     (2, 37, 45, 16, 0, 16),     # ragged edges on both axes
+    (1, 17, 36, 8, 0, 8),       # 8 -> 8 row pairs: odd height (the last pair's second row is padding)
+    (1, 33, 40, 8, 8, 8),       # 8 + 8 -> 8 row pairs (C = 16: 6 k-steps), odd height
+    (2, 3, 20, 16, 0, 8),       # one partial tile, rows past Ho inside the first pair
 ]
 
 
