@@ -133,6 +133,13 @@ typedef struct {
      * n a multiple of 64 and the float4 epilogue runs as 16 element-wise GEMMs over the transformed
      * tiles (2.25x fewer products; same 6-product fp32 arithmetic, fp32 transforms) */
     const void* wino;
+    /* optional: per-(image, output channel) factors [batch][chan_scale_ld] (fp32, 16-byte aligned,
+     * chan_scale_ld % 4 == 0; 0 -> n, or n/4 under SHUFFLE2).  The epilogue multiplies column n
+     * (SHUFFLE2: output channel c) of image b by chan_scale[b * ld + n] after the mask and before
+     * ACCUM: the Dropout2d channel scale (unet_p_res.py:62, :69; x * mask / (1 - p)) applied by
+     * the conv that produces the tensor instead of a separate pass over it - the same product as
+     * pu_channel_scale.  fp32 entry point only (pu_conv_igemm_bf16 rejects it). */
+    const float* chan_scale; int chan_scale_ld;
 } pu_conv_args;
 
 int pu_conv_igemm(const pu_conv_args* a, void* stream);

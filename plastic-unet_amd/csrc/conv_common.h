@@ -1,7 +1,8 @@
 // Types and epilogue helpers shared by the fp32 implicit-GEMM kernels (igemm.hip) and the
 // Winograd F(2x2,3x3) kernel (winograd.hip): the launch parameters, the float4 output epilogue
 // (bias / residual / ReLU / mask / concat split / accumulate / ConvT shuffle) and the exact
-// 3-term bf16 split of fp32 operands.
+// 3-term bf16 split of fp32 operands.  Epilogue order: bias, residual, ReLU, mask, channel scale,
+// accumulate.
 #pragma once
 #include "common.h"
 
@@ -31,22 +32,27 @@ struct IgemmParams {
     int shuf_h, shuf_w, shuf_off;   // SHUFFLE2 output grid and crop offset
     FastDiv dWo, dHo, dC, dKw, dCo, dTaps;
     int in_pix;             // batch * Hi * Wi (lean kernel's buffer extent)
+    const float* cscale;    // per-(image, channel) factors [batch][cs_ld] or null (chan_scale)
+    int cs_ld;
+    FastDiv dHW;            // Ho * Wo: the image of GEMM row m
 };
 
 // Output position of GEMM row m: the pixel itself, or (SHUFFLE2) the batch row base b*shuf_h and
-// the top-left corner (2ho - off, 2wo - off) of its 2x2 output block.
+// the top-left corner (2ho - off, 2wo - off) of its 2x2 output block; b = the image (formed only
+// when a channel scale needs it).
 struct EpiRow {
     long long pix;
     int oh0, ow0;
+    int b;
 };
 
 __device__ __forceinline__ EpiRow epi_row(const IgemmParams& p, int m) {
-    if (!(p.flags & PU_EPI_SHUFFLE2)) return {m, 0, 0};
+    if (!(p.flags & PU_EPI_SHUFFLE2)) return {m, 0, 0, p.cscale ? (int)fdiv(m, p.dHW) : 0};
     const int t2 = fdiv(m, p.dWo);
     const int wo = m - t2 * p.Wo;
     const int bb = fdiv(t2, p.dHo);
     const int ho = t2 - bb * p.Ho;
-    return {(long long)bb * p.shuf_h, 2 * ho - p.shuf_off, 2 * wo - p.shuf_off};
+    return {(long long)bb * p.shuf_h, 2 * ho - p.shuf_off, 2 * wo - p.shuf_off, bb};
 }
 
 // SHUFFLE2 destination element offset of channel n of row r; false if cropped away
@@ -88,6 +94,7 @@ __device__ __forceinline__ void epi_store4(const IgemmParams& p, const EpiRow& r
 #pragma unroll
         for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
     }
+    if (p.cscale) v *= *reinterpret_cast<const f32x4*>(p.cscale + (long long)r.b * p.cs_ld + nb);
     if (p.flags & PU_EPI_ACCUM) v += *reinterpret_cast<const f32x4*>(dst + off);
     *reinterpret_cast<f32x4*>(dst + off) = v;
 }

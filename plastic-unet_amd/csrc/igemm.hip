@@ -113,6 +113,7 @@ __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM 
                         float v = acc[i][j][4 * q + e] + (p.bias ? p.bias[bi] : 0.f) + (p.resid ? p.resid[o] : 0.f);
                         if (relu) v = fmaxf(v, 0.f);
                         if (mk && !(mk[o] > 0.f)) v = 0.f;
+                        if (p.cscale) v *= p.cscale[(long long)er.b * p.cs_ld + bi];
                         if (accum) v += d[o];
                         d[o] = v;
                     }
@@ -1332,6 +1333,13 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
     p.cgroup = a->cgroup;
     p.vec_epi = vec_epilogue(a);
     p.in_pix = a->batch * a->in_h * a->in_w;
+    p.cscale = a->chan_scale;
+    p.cs_ld = a->chan_scale_ld ? a->chan_scale_ld : (shuffle ? a->n / 4 : a->n);
+    p.dHW = make_fastdiv(a->out_h * a->out_w);
+    if (a->chan_scale) {
+        PU_REQUIRE(((uintptr_t)a->chan_scale & 15) == 0 && p.cs_ld % 4 == 0 && p.cs_ld >= (shuffle ? a->n / 4 : a->n),
+                   "pu_conv_igemm: chan_scale must be 16-byte aligned with a row stride >= its channels and %% 4 == 0 (ld %d)", p.cs_ld);
+    }
 
     const int mode = choose_mode(a->c0, a->c1);
     PU_REQUIRE(a->cgroup == 0 || a->cgroup == 16 || a->cgroup == 32, "pu_conv_igemm: cgroup %d", a->cgroup);

@@ -435,6 +435,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 #pragma unroll
                             for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
                         }
+                        if (p.cscale) v *= *reinterpret_cast<const f32x4*>(p.cscale + (long long)b * p.cs_ld + n);
                         if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
                         *reinterpret_cast<f32x4*>(dst + off) = v;
                     }

@@ -34,7 +34,7 @@ class ConvArgs(ctypes.Structure):
                 ("dst0", P), ("n0", c_int), ("dst1", P), ("mask0", P), ("mask1", P), ("flags", c_int),
                 ("workspace", P), ("ws_bytes", c_size),
                 ("resid", P), ("shuf_h", c_int), ("shuf_w", c_int), ("shuf_off", c_int),
-                ("weight6", P), ("wino", P)]
+                ("weight6", P), ("wino", P), ("chan_scale", P), ("chan_scale_ld", c_int)]
 
 
 class WgradArgs(ctypes.Structure):

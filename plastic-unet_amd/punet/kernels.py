@@ -216,20 +216,27 @@ def cgroup_for(c0, c1=0):
 
 def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, dst0, n0=None,
           src1=None, c1=0, bias=None, dst1=None, mask0=None, mask1=None, relu=False, accum=False,
-          shuffle=False, cgroup=0, resid=None, shuf=(0, 0, 0)):
+          shuffle=False, cgroup=0, resid=None, shuf=(0, 0, 0), chan_scale=None):
     """pu_conv_igemm: implicit-GEMM conv (3x3 fwd/dgrad, ConvT fwd with shuffle, ConvT dgrad).
-    resid: residual tensor added before ReLU/mask; shuf = (out_h, out_w, crop) of a SHUFFLE2 grid."""
+    resid: residual tensor added before ReLU/mask; shuf = (out_h, out_w, crop) of a SHUFFLE2 grid;
+    chan_scale: [batch, ld] per-(image, column) factors applied after the mask (the Dropout2d scale
+    of the tensor being produced; SHUFFLE2: per output channel)."""
     dt = _act_dtype(src0)
     for t, nm in ((src0, "src0"), (src1, "src1"), (weight, "weight"), (dst0, "dst0"),
                   (dst1, "dst1"), (mask0, "mask0"), (mask1, "mask1"), (resid, "resid")):
         _req(t, nm, dt)
     _req(bias, "bias")
+    _req(chan_scale, "chan_scale")
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
         | (PU_EPI_RESID if resid is not None else 0) | _halo_flags() | (0 if _SMALLX6 else PU_CONV_NO_SMALLX6)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,
                  _p(resid), shuf[0], shuf[1], shuf[2])
+    if chan_scale is not None:
+        if chan_scale.dim() != 2 or chan_scale.shape[0] != batch:
+            raise RuntimeError("chan_scale must be [batch, channels]")
+        a.chan_scale, a.chan_scale_ld = chan_scale.data_ptr(), chan_scale.shape[1]
     w6 = getattr(weight, "_split6", None) if (dt != BF16 and _FP32_MATH == "split6") else None
     if w6 is not None:
         a.weight6 = w6.data_ptr()

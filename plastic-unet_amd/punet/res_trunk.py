@@ -45,8 +45,9 @@ def conv3x3(x0, w, b, packs, x1=None, relu=True, resid=None):
     return out
 
 
-def conv3x3_dgrad(dz, w, packs, split=None, mask0=None, mask1=None, resid=None):
-    """dX = conv(dZ, flipped W^T) (+ resid) (. mask); optional channel split -> (d0, d1)."""
+def conv3x3_dgrad(dz, w, packs, split=None, mask0=None, mask1=None, resid=None, chan_scale=None):
+    """dX = conv(dZ, flipped W^T) (+ resid) (. mask) (* chan_scale[b, c]: the Dropout2d backward);
+    optional channel split -> (d0, d1)."""
     B, H, W, cout = dz.shape
     cin = w.shape[1]
     k_pad = K.round16(9 * cout)
@@ -56,7 +57,7 @@ def conv3x3_dgrad(dz, w, packs, split=None, mask0=None, mask1=None, resid=None):
     d1 = None if split is None else torch.empty(B, H, W, cin - n0, dtype=torch.float32, device=dz.device)
     K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=dz, c0=cout,
             weight=packs.get(w, PU_PACK_CONV_DGRAD, k_pad, g), k_pad=k_pad, n=cin, dst0=d0, n0=n0, dst1=d1,
-            mask0=mask0, mask1=mask1, cgroup=g, resid=resid)
+            mask0=mask0, mask1=mask1, cgroup=g, resid=resid, chan_scale=chan_scale)
     return d0, d1
 
 
@@ -82,8 +83,17 @@ def _crop(h, out_h):
     return crop
 
 
-def convT3x3(x, w, b, packs, out_hw):
-    """ConvTranspose2d(cin, cout, 3, stride=2, padding=0) + crop to out_hw (NHWC)."""
+def _fusable(m):
+    """A Dropout2d mask the conv epilogue can apply (float4 rows: width % 4 == 0, 16-byte aligned
+    contiguous rows), else None (a separate pu_channel_scale pass)."""
+    if m is None or m.shape[1] % 4 or not m.is_contiguous() or m.data_ptr() % 16:
+        return None
+    return m
+
+
+def convT3x3(x, w, b, packs, out_hw, chan_scale=None):
+    """ConvTranspose2d(cin, cout, 3, stride=2, padding=0) + crop to out_hw (NHWC); chan_scale
+    [B, >= cout] (row stride = its width): per-(image, channel) factors (the Dropout2d of up())."""
     B, h, wd, cin = x.shape
     cout = w.shape[1]
     H2, W2 = out_hw
@@ -94,7 +104,7 @@ def convT3x3(x, w, b, packs, out_hw):
     out = torch.empty(B, H2, W2, cout, dtype=torch.float32, device=x.device)
     K.igemm(batch=B, in_hw=(h, wd), out_hw=(h + 1, wd + 1), k=2, stride=1, pad=1, src0=x, c0=cin,
             weight=packs.get(w, PU_PACK_CONVT3_FWD, k_pad), k_pad=k_pad, n=4 * cout, bias=b, dst0=out,
-            shuffle=True, shuf=(H2, W2, crop))
+            shuffle=True, shuf=(H2, W2, crop), chan_scale=chan_scale)
     return out
 
 
@@ -276,13 +286,17 @@ class ResTrunk:
         for j, name in enumerate(self.UP):
             skip = skips[3 - j]
             i = self.slots[name + ".up"]
-            u = convT3x3(y, P[i], P[i + 1], self.packs, skip.shape[1:3])
+            # Dropout2d over cat(u, skip) (unet_p_res.py:69): u's channels scaled by the ConvT
+            # epilogue (the mask's row stride spans both parts), the skip's by a scaled copy (the
+            # unscaled skip stays for MaxPool2d's backward)
+            m = self._mask(name, y.shape[0], P[i].shape[1] + skip.shape[3], p_drop, y.device) if drop else None
+            u = convT3x3(y, P[i], P[i + 1], self.packs, skip.shape[1:3], chan_scale=_fusable(m))
             s[name + ".in"] = y
             src1 = skip
             if drop:
                 cu = u.shape[3]
-                m = self._mask(name, u.shape[0], cu + skip.shape[3], p_drop, u.device)
-                K.channel_scale(u, m[:, :cu].contiguous(), out=u)
+                if _fusable(m) is None:
+                    K.channel_scale(u, m[:, :cu].contiguous(), out=u)
                 src1 = K.channel_scale(skip, m[:, cu:].contiguous())
                 s[name + ".mask"] = m
             y, st = self._stack_fwd(P, self.slots[name], u, src1)
@@ -295,7 +309,7 @@ class ResTrunk:
         return logits, (s if save else None)
 
     # --------------------------------------------------------------------------- backward
-    def _stack_bwd(self, P, i, st, g, grads, out, need_dx=True, split=None, mask1=None):
+    def _stack_bwd(self, P, i, st, g, grads, out, need_dx=True, split=None, mask1=None, chan_scale=None):
         pk = self.packs
         x0, x1, r1, a1, r2, a2, y = st
         dbg = self.debug
@@ -317,7 +331,7 @@ class ResTrunk:
             dbg[i] = (g, g_a2, g_o1, g_a1, g_z0)
         if not need_dx:
             return None, None
-        return conv3x3_dgrad(g_z0, P[i], pk, split=split, mask1=mask1)
+        return conv3x3_dgrad(g_z0, P[i], pk, split=split, mask1=mask1, chan_scale=chan_scale)
 
     def _bn_bwd(self, P, key, z, g, stat, out, grads, add=None, mask=None):
         j, _ = self.bn[key]
@@ -372,9 +386,11 @@ class ResTrunk:
             st = s[name]
             cu = st[0].shape[3]
             skip = skips[3 - j]
-            g_u, g_sk = self._stack_bwd(P, self.slots[name], st, g, grads, out, split=cu, mask1=skip)
+            # the Dropout2d backward of cat(u, skip) in the split data gradient's epilogue
             m = s.get(name + ".mask")
-            if m is not None:
+            g_u, g_sk = self._stack_bwd(P, self.slots[name], st, g, grads, out, split=cu, mask1=skip,
+                                        chan_scale=_fusable(m))
+            if m is not None and _fusable(m) is None:
                 K.channel_scale(g_u, m[:, :cu].contiguous(), out=g_u)
                 K.channel_scale(g_sk, m[:, cu:].contiguous(), out=g_sk)
             gskip[3 - j] = g_sk

@@ -104,6 +104,39 @@ def test_channel_scale_and_column_sum():
         assert torch.equal(s, again)                # fixed order: bitwise reproducible
 
 
+@pytest.mark.parametrize("B,H,cout,cin,split", [
+    (2, 20, 8, 16, 8),       # 8 -> 8 + 8: small-channel MFMA kernel
+    (2, 18, 32, 32, 16),     # 32 -> 16 + 16: lean x6 tile
+    (2, 16, 64, 128, 64),    # 64 -> 64 + 64: Winograd
+    (1, 8, 64, 128, 64),     # 8x8 grid: Winograd with split-K (the split epilogue kernel)
+    (2, 9, 16, 6, 3),        # 3 + 3 channels: the per-element epilogue
+])
+def test_fused_dropout_scale_in_conv_epilogue(B, H, cout, cin, split):
+    """chan_scale (the Dropout2d factors of cat(u, skip), row stride >= the output channels) in the
+    split data gradient's epilogue and in the ConvT forward's shuffled epilogue: bitwise equal to
+    the separate pu_channel_scale pass over the unscaled outputs."""
+    g = torch.Generator().manual_seed(B * 100 + H + cin)
+    pk = R._Packs()
+    dz = nhwc(rnd(B, cout, H, H, g=g)).to(DEV)
+    w = rnd(cout, cin, 3, 3, g=g, scale=0.2).to(DEV)
+    skip = nhwc(rnd(B, cin - split, H, H, g=g).relu()).to(DEV)
+    ld = (cin + 3) // 4 * 4
+    m = ((torch.rand(B, ld, generator=g) >= 0.5).float() * 2.0).to(DEV)
+    d0, d1 = R.conv3x3_dgrad(dz, w, pk, split=split, mask1=skip)
+    f0, f1 = R.conv3x3_dgrad(dz, w, pk, split=split, mask1=skip, chan_scale=m)
+    assert torch.equal(f0, K.channel_scale(d0, m[:, :split].contiguous()))
+    assert torch.equal(f1, K.channel_scale(d1, m[:, split:cin].contiguous()))
+    # ConvT 3x3 s2 forward (SHUFFLE2): factors per output channel, row stride of the concat mask
+    h = H // 2
+    x = nhwc(rnd(B, cin, h, h, g=g)).to(DEV)
+    wt = rnd(cin, cout, 3, 3, g=g, scale=0.2).to(DEV)
+    b = rnd(cout, g=g).to(DEV)
+    mt = ((torch.rand(B, cout + 8, generator=g) >= 0.5).float() * 2.0).to(DEV)
+    u = R.convT3x3(x, wt, b, pk, (2 * h, 2 * h))
+    uf = R.convT3x3(x, wt, b, pk, (2 * h, 2 * h), chan_scale=mt)
+    assert torch.equal(uf, K.channel_scale(u, mt[:, :cout].contiguous()))
+
+
 def _load(net, g, prefix):
     net.load_state_dict({k[len(prefix):]: torch.from_numpy(np.asarray(v)) for k, v in g.items()
                          if k.startswith(prefix)})
