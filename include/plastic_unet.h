@@ -291,6 +291,12 @@ int pu_column_sum(const float* x, long long rows, int cols, float* out, int accu
 int pu_maxpool2_fwd(const float* x, float* y, int batch, int h, int w, int c, void* stream);
 int pu_maxpool2_bwd(const float* x, const float* dy, float* dx, int batch, int h, int w, int c,
                     int relu_mask, int accumulate, void* stream);
+/* The same with the Dropout2d that follows the pool (unet_p_res.py:62, pool_drop): fwd writes
+ * maxpool(x) * scale[b][c]; bwd routes dy * scale[b][c] (the dropout's backward) - the products
+ * pu_channel_scale computes, without its pass over the pooled tensor.  scale: [batch][c] fp32. */
+int pu_maxpool2_fwd_scaled(const float* x, const float* scale, float* y, int batch, int h, int w, int c, void* stream);
+int pu_maxpool2_bwd_scaled(const float* x, const float* dy, const float* scale, float* dx, int batch, int h, int w,
+                           int c, int relu_mask, int accumulate, void* stream);
 
 /* outconv (1x1, C -> 1): y[m] = b + sum_c x[m][c]*w[c].
  * bwd: dx[m][c] = dy[m]*w[c]*(relu_mask ? x[m][c] > 0 : 1); dw[c] = sum_m dy[m]x[m][c];

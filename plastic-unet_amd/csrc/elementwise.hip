@@ -201,7 +201,7 @@ __device__ __forceinline__ void pool_take(float v, int idx, float& best, int& ar
 
 template <bool VEC, typename T = float>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int H, int W, int C, int Ho,
-                                   int Wo, long long total) {
+                                   int Wo, long long total, const float* __restrict__ scale) {
     const int CV = VEC ? C / 4 : C;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * blockDim.x) {
@@ -221,6 +221,7 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, i
 #pragma unroll
                 for (int e = 0; e < 4; ++e) { float bb = best[e]; pool_take(v[e], q, bb, arg[e]); best[e] = bb; }
             }
+            if (scale) best *= ld4(scale + b * C + cv * 4);
             st4(y + idx * 4, best);
         } else {
             float best = -INFINITY;
@@ -230,6 +231,7 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, i
                 const long long pix = base + (q >> 1) * W + (q & 1);
                 pool_take((float)x[pix * C + cv], q, best, arg);
             }
+            if (scale) best *= scale[b * C + cv];
             y[idx] = (T)best;
         }
     }
@@ -240,7 +242,7 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, i
 template <bool VEC, typename T = float>
 __global__ void maxpool_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
                                    int H, int W, int C, int Ho, int Wo, int relu_mask, int accumulate,
-                                   long long total) {
+                                   long long total, const float* __restrict__ scale) {
     constexpr int V = VEC ? 4 : 1;
     const int CV = C / V;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -280,7 +282,8 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ x, const T* __restrict_
             const long long oidx = ((b * Ho + ho) * Wo + wo) * C + cv * V;
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                if (arg[e] == me && (!relu_mask || xme[e] > 0.f)) out[e] = (float)dy[oidx + e];
+                if (arg[e] == me && (!relu_mask || xme[e] > 0.f))
+                    out[e] = scale ? (float)dy[oidx + e] * scale[b * C + cv * V + e] : (float)dy[oidx + e];
             }
         }
 #pragma unroll
@@ -328,7 +331,7 @@ __device__ __forceinline__ void st16(T* p, const float (&v)[Vec16<T>::V]) {
 // instead of one thread per full-resolution pixel re-reading the whole window.
 template <typename T>
 __global__ void maxpool_fwd_win_kernel(const T* __restrict__ x, T* __restrict__ y, int W, int C, int Ho, int Wo,
-                                       long long total) {
+                                       long long total, const float* __restrict__ scale) {
     constexpr int V = Vec16<T>::V;
     const int CV = C / V;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -349,13 +352,18 @@ __global__ void maxpool_fwd_win_kernel(const T* __restrict__ x, T* __restrict__ 
 #pragma unroll
             for (int e = 0; e < V; ++e) pool_take(v.v[e], q, best[e], arg[e]);
         }
+        if (scale) {            // Dropout2d after the pool (unet_p_res.py:62): the pooled value times s[b][c]
+#pragma unroll
+            for (int e = 0; e < V; ++e) best[e] *= scale[b * C + cv * V + e];
+        }
         st16(y + idx * V, best);
     }
 }
 
 template <typename T>
 __global__ void maxpool_bwd_win_kernel(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx, int W,
-                                       int C, int Ho, int Wo, int relu_mask, int accumulate, long long total) {
+                                       int C, int Ho, int Wo, int relu_mask, int accumulate, long long total,
+                                       const float* __restrict__ scale) {
     constexpr int V = Vec16<T>::V;
     const int CV = C / V;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -377,7 +385,11 @@ __global__ void maxpool_bwd_win_kernel(const T* __restrict__ x, const T* __restr
 #pragma unroll
             for (int e = 0; e < V; ++e) pool_take(xv[q].v[e], q, best[e], arg[e]);
         }
-        const Vec16<T> g = ld16(dy + idx * V);
+        Vec16<T> g = ld16(dy + idx * V);
+        if (scale) {            // the Dropout2d backward of the pooled gradient
+#pragma unroll
+            for (int e = 0; e < V; ++e) g.v[e] *= scale[b * C + cv * V + e];
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             T* d = dx + (base + (q >> 1) * W + (q & 1)) * C + cv * V;
@@ -770,45 +782,67 @@ extern "C" int pu_nchw_to_nhwc(const float* src, float* dst, int batch, int c, i
     return check_launch("pu_nchw_to_nhwc");
 }
 
-extern "C" int pu_maxpool2_fwd(const float* x, float* y, int batch, int h, int w, int c, void* stream) {
+static int maxpool2_fwd_f32(const float* x, float* y, const float* scale, int batch, int h, int w, int c, void* stream) {
     PU_REQUIRE(x && y && batch > 0 && h >= 2 && w >= 2 && c > 0, "pu_maxpool2_fwd: bad args");
     const int ho = h / 2, wo = w / 2;
     const bool vec = (c % 4 == 0) && (((uintptr_t)x | (uintptr_t)y) & 15) == 0;
     if (vec && h % 2 == 0 && w % 2 == 0) {
         const long long wt = (long long)batch * ho * wo * (c / 4);
         hipLaunchKernelGGL(maxpool_fwd_win_kernel<float>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream), x, y, w, c,
-                           ho, wo, wt);
+                           ho, wo, wt, scale);
         return check_launch("pu_maxpool2_fwd");
     }
-    const long long total = (long long)batch * ho * wo * (vec ? c / 4 : c);
-    if (vec)
+    const bool vs = vec && ((uintptr_t)scale & 15) == 0;
+    const long long total = (long long)batch * ho * wo * (vs ? c / 4 : c);
+    if (vs)
         hipLaunchKernelGGL(maxpool_fwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, y, h, w,
-                           c, ho, wo, total);
+                           c, ho, wo, total, scale);
     else
         hipLaunchKernelGGL(maxpool_fwd_kernel<false>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, y, h,
-                           w, c, ho, wo, total);
+                           w, c, ho, wo, total, scale);
     return check_launch("pu_maxpool2_fwd");
 }
 
-extern "C" int pu_maxpool2_bwd(const float* x, const float* dy, float* dx, int batch, int h, int w, int c,
-                               int relu_mask, int accumulate, void* stream) {
+extern "C" int pu_maxpool2_fwd(const float* x, float* y, int batch, int h, int w, int c, void* stream) {
+    return maxpool2_fwd_f32(x, y, nullptr, batch, h, w, c, stream);
+}
+
+extern "C" int pu_maxpool2_fwd_scaled(const float* x, const float* scale, float* y, int batch, int h, int w, int c,
+                                      void* stream) {
+    PU_REQUIRE(scale, "pu_maxpool2_fwd_scaled: scale missing");
+    return maxpool2_fwd_f32(x, y, scale, batch, h, w, c, stream);
+}
+
+static int maxpool2_bwd_f32(const float* x, const float* dy, const float* scale, float* dx, int batch, int h, int w,
+                            int c, int relu_mask, int accumulate, void* stream) {
     PU_REQUIRE(x && dy && dx && batch > 0 && h >= 2 && w >= 2 && c > 0, "pu_maxpool2_bwd: bad args");
     const int ho = h / 2, wo = w / 2;
     const bool vec = (c % 4 == 0);
     if (vec && h % 2 == 0 && w % 2 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) == 0) {
         const long long wt = (long long)batch * ho * wo * (c / 4);
         hipLaunchKernelGGL(maxpool_bwd_win_kernel<float>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream), x, dy, dx,
-                           w, c, ho, wo, relu_mask, accumulate, wt);
+                           w, c, ho, wo, relu_mask, accumulate, wt, scale);
         return check_launch("pu_maxpool2_bwd");
     }
     const long long total = (long long)batch * h * w * (vec ? c / 4 : c);
     if (vec)
         hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, dy, dx,
-                           h, w, c, ho, wo, relu_mask, accumulate, total);
+                           h, w, c, ho, wo, relu_mask, accumulate, total, scale);
     else
         hipLaunchKernelGGL(maxpool_bwd_kernel<false>, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x, dy, dx,
-                           h, w, c, ho, wo, relu_mask, accumulate, total);
+                           h, w, c, ho, wo, relu_mask, accumulate, total, scale);
     return check_launch("pu_maxpool2_bwd");
+}
+
+extern "C" int pu_maxpool2_bwd(const float* x, const float* dy, float* dx, int batch, int h, int w, int c,
+                               int relu_mask, int accumulate, void* stream) {
+    return maxpool2_bwd_f32(x, dy, nullptr, dx, batch, h, w, c, relu_mask, accumulate, stream);
+}
+
+extern "C" int pu_maxpool2_bwd_scaled(const float* x, const float* dy, const float* scale, float* dx, int batch, int h,
+                                      int w, int c, int relu_mask, int accumulate, void* stream) {
+    PU_REQUIRE(scale, "pu_maxpool2_bwd_scaled: scale missing");
+    return maxpool2_bwd_f32(x, dy, scale, dx, batch, h, w, c, relu_mask, accumulate, stream);
 }
 
 extern "C" int pu_outconv_fwd(const float* x, const float* w, const float* b, float* y, long long rows, int c,
@@ -926,12 +960,12 @@ extern "C" int pu_maxpool2_fwd_bf16(const void* x, void* y, int batch, int h, in
     if (c % 8 == 0 && h % 2 == 0 && w % 2 == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
         const long long wt = (long long)batch * ho * wo * (c / 8);
         hipLaunchKernelGGL(maxpool_fwd_win_kernel<__bf16>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream),
-                           (const __bf16*)x, (__bf16*)y, w, c, ho, wo, wt);
+                           (const __bf16*)x, (__bf16*)y, w, c, ho, wo, wt, nullptr);
         return check_launch("pu_maxpool2_fwd_bf16");
     }
     const long long total = (long long)batch * ho * wo * (c / 4);
     hipLaunchKernelGGL((maxpool_fwd_kernel<true, __bf16>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
-                       (const __bf16*)x, (__bf16*)y, h, w, c, ho, wo, total);
+                       (const __bf16*)x, (__bf16*)y, h, w, c, ho, wo, total, nullptr);
     return check_launch("pu_maxpool2_fwd_bf16");
 }
 
@@ -942,12 +976,14 @@ extern "C" int pu_maxpool2_bwd_bf16(const void* x, const void* dy, void* dx, int
     if (c % 8 == 0 && h % 2 == 0 && w % 2 == 0 && (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) == 0) {
         const long long wt = (long long)batch * ho * wo * (c / 8);
         hipLaunchKernelGGL(maxpool_bwd_win_kernel<__bf16>, dim3(grid_for(wt)), dim3(256), 0, as_stream(stream),
-                           (const __bf16*)x, (const __bf16*)dy, (__bf16*)dx, w, c, ho, wo, relu_mask, accumulate, wt);
+                           (const __bf16*)x, (const __bf16*)dy, (__bf16*)dx, w, c, ho, wo, relu_mask, accumulate, wt,
+                           nullptr);
         return check_launch("pu_maxpool2_bwd_bf16");
     }
     const long long total = (long long)batch * h * w * (c / 4);
     hipLaunchKernelGGL((maxpool_bwd_kernel<true, __bf16>), dim3(grid_for(total)), dim3(256), 0, as_stream(stream),
-                       (const __bf16*)x, (const __bf16*)dy, (__bf16*)dx, h, w, c, ho, wo, relu_mask, accumulate, total);
+                       (const __bf16*)x, (const __bf16*)dy, (__bf16*)dx, h, w, c, ho, wo, relu_mask, accumulate, total,
+                       nullptr);
     return check_launch("pu_maxpool2_bwd_bf16");
 }
 

@@ -116,6 +116,8 @@ SIGNATURES = [
     ("pu_column_sum", c_int, [P, c_ll, c_int, P, c_int, P, c_size, P]),
     ("pu_maxpool2_fwd", c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     ("pu_maxpool2_bwd", c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    ("pu_maxpool2_fwd_scaled", c_int, [P, P, P, c_int, c_int, c_int, c_int, P]),
+    ("pu_maxpool2_bwd_scaled", c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     ("pu_outconv_fwd", c_int, [P, P, P, P, c_ll, c_int, P]),
     ("pu_outconv_workspace_bytes", c_size, [c_ll, c_int]),
     ("pu_outconv_bwd", c_int, [P, P, P, P, P, P, c_ll, c_int, c_int, P, c_size, P]),

@@ -466,25 +466,37 @@ def column_sum(x2d, out=None, accumulate=False):
     return out
 
 
-def maxpool2_fwd(x):
+def maxpool2_fwd(x, scale=None):
+    """MaxPool2d(2); scale [B, C] (fp32 only): the Dropout2d that follows the pool, fused."""
     dt = _act_dtype(x)
     _req(x, "x", dt)
     B, H, W, C = x.shape
     y = torch.empty(B, H // 2, W // 2, C, dtype=dt, device=x.device)
-    fn = lib().pu_maxpool2_fwd_bf16 if dt == BF16 else lib().pu_maxpool2_fwd
     with _Rec("maxpool_fwd", nbytes=x.element_size() * (x.numel() + y.numel())):
-        check(fn(x.data_ptr(), y.data_ptr(), B, H, W, C, _stream()), "pu_maxpool2_fwd")
+        if scale is not None:
+            _req(x, "x"); _req(scale, "scale")       # fp32 entry point
+            check(lib().pu_maxpool2_fwd_scaled(x.data_ptr(), scale.data_ptr(), y.data_ptr(), B, H, W, C, _stream()),
+                  "pu_maxpool2_fwd_scaled")
+        else:
+            fn = lib().pu_maxpool2_fwd_bf16 if dt == BF16 else lib().pu_maxpool2_fwd
+            check(fn(x.data_ptr(), y.data_ptr(), B, H, W, C, _stream()), "pu_maxpool2_fwd")
     return y
 
 
-def maxpool2_bwd(x, dy, dx, relu_mask=True, accumulate=True):
+def maxpool2_bwd(x, dy, dx, relu_mask=True, accumulate=True, scale=None):
+    """MaxPool2d(2) backward; scale [B, C] (fp32 only): dy * scale routed (the Dropout2d backward)."""
     dt = _act_dtype(x)
     _req(x, "x", dt); _req(dy, "dy", dt); _req(dx, "dx", dt)
     B, H, W, C = x.shape
-    fn = lib().pu_maxpool2_bwd_bf16 if dt == BF16 else lib().pu_maxpool2_bwd
     with _Rec("maxpool_bwd", nbytes=x.element_size() * (x.numel() * (3 if accumulate else 2) + dy.numel())):
-        check(fn(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C, int(relu_mask), int(accumulate), _stream()),
-              "pu_maxpool2_bwd")
+        if scale is not None:
+            _req(x, "x"); _req(scale, "scale")       # fp32 entry point
+            check(lib().pu_maxpool2_bwd_scaled(x.data_ptr(), dy.data_ptr(), scale.data_ptr(), dx.data_ptr(), B, H, W,
+                                               C, int(relu_mask), int(accumulate), _stream()), "pu_maxpool2_bwd_scaled")
+        else:
+            fn = lib().pu_maxpool2_bwd_bf16 if dt == BF16 else lib().pu_maxpool2_bwd
+            check(fn(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), B, H, W, C, int(relu_mask), int(accumulate),
+                     _stream()), "pu_maxpool2_bwd")
     return dx
 
 

@@ -272,11 +272,10 @@ class ResTrunk:
                 y, st = self._stack_fwd(P, self.slots[name], h)
             s[name] = st
             skips.append(y)
-            h = K.maxpool2_fwd(y)
             p = p_drop / 2 if k == 0 else p_drop          # pool1 uses dropout_ratio/2 (:39)
+            m = self._mask("pool%d" % (k + 1), y.shape[0], y.shape[3], p, y.device) if drop else None
+            h = K.maxpool2_fwd(y, scale=m)                # pool_drop (:62): the Dropout2d fused
             if drop:
-                m = self._mask("pool%d" % (k + 1), h.shape[0], h.shape[3], p, h.device)
-                K.channel_scale(h, m, out=h)
                 s["pool%d.mask" % (k + 1)] = m
         if ("mid", 1) in self.bn:
             y, st = self._stack_fwd_bn(P, self.slots["mid"], "mid", h)
@@ -404,10 +403,8 @@ class ResTrunk:
         else:
             g_p, _ = self._stack_bwd(P, self.slots["mid"], s["mid"], g, grads, out)
         for k in range(3, -1, -1):                       # conv4 .. conv1
-            m = s.get("pool%d.mask" % (k + 1))
-            if m is not None:
-                K.channel_scale(g_p, m, out=g_p)
-            g = K.maxpool2_bwd(skips[k], g_p, gskip[k], relu_mask=True, accumulate=True)
+            g = K.maxpool2_bwd(skips[k], g_p, gskip[k], relu_mask=True, accumulate=True,
+                               scale=s.get("pool%d.mask" % (k + 1)))
             name = self.DOWN[k]
             if (name, 1) in self.bn:
                 g_p, _ = self._stack_bwd_bn(P, self.slots[name], name, s[name], g, grads, out, need_dx=k > 0)

@@ -137,6 +137,23 @@ def test_fused_dropout_scale_in_conv_epilogue(B, H, cout, cin, split):
     assert torch.equal(uf, K.channel_scale(u, mt[:, :cout].contiguous()))
 
 
+@pytest.mark.parametrize("B,H,W,C", [(2, 16, 24, 8), (3, 9, 13, 16), (2, 8, 8, 6)])
+def test_maxpool_with_fused_dropout_scale(B, H, W, C):
+    """pool_drop (unet_p_res.py:62) with the Dropout2d in the pool kernels: forward = maxpool then
+    the per-(image, channel) factor, backward = the factor on dy routed to the argmax - bitwise the
+    separate pu_channel_scale pass (even / odd sizes, vector and per-element paths)."""
+    g = torch.Generator().manual_seed(B * 31 + H + C)
+    x = nhwc(rnd(B, C, H, W, g=g)).to(DEV)
+    m = ((torch.rand(B, C, generator=g) >= 0.5).float() * 2.0).to(DEV)
+    y = K.maxpool2_fwd(x, scale=m)
+    assert torch.equal(y, K.channel_scale(K.maxpool2_fwd(x), m))
+    dy = rnd(*y.shape, g=g).to(DEV)
+    base = rnd(*x.shape, g=g).to(DEV)
+    d1 = K.maxpool2_bwd(x, dy, base.clone(), relu_mask=True, accumulate=True, scale=m)
+    d2 = K.maxpool2_bwd(x, K.channel_scale(dy, m), base.clone(), relu_mask=True, accumulate=True)
+    assert torch.equal(d1, d2)
+
+
 def _load(net, g, prefix):
     net.load_state_dict({k[len(prefix):]: torch.from_numpy(np.asarray(v)) for k, v in g.items()
                          if k.startswith(prefix)})
