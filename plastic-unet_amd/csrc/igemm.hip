@@ -1074,7 +1074,8 @@ __global__ __launch_bounds__(256) void conv1x1_small_kernel(const IgemmParams p)
 }
 
 // ---------------------------------------------------------------- single-channel stem (C = 1)
-// The first 3x3 conv (inc.c0: 1 -> N channels, unet_p.py:208-215) is a K = 9 GEMM: nothing for
+// The first 3x3 conv (inc.c0: 1 -> N channels, N in {8, 16, 32, 64}; unet_p.py:208-215, the
+// 8/16-channel stems of C4/C5) is a K = 9 GEMM: nothing for
 // an MFMA tile to do, the layer is the write of its N-channel output.  A block stages the 1-channel
 // halo of a 16 x 64 pixel tile in LDS; lanes work in groups of L = N/4 per pixel, each lane 4
 // output channels (36 weights in registers), so every wave-instruction of the shared float4
@@ -1271,7 +1272,7 @@ static bool small_conv_ok(const pu_conv_args* a) {
 // groups that divide a wave), plain (non-SHUFFLE2) float4 epilogue
 static bool stem_conv_ok(const pu_conv_args* a) {
     const int C = a->c0 + a->c1;
-    return C == 1 && a->c1 == 0 && (a->n == 32 || a->n == 64) && a->kh == 3 && a->kw == 3 && a->stride == 1 &&
+    return C == 1 && a->c1 == 0 && (a->n == 8 || a->n == 16 || a->n == 32 || a->n == 64) && a->kh == 3 && a->kw == 3 && a->stride == 1 &&
            a->pad == 1 && a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) &&
            vec_epilogue(a) && (a->cgroup == 0 || a->cgroup >= C);
 }
@@ -1357,7 +1358,9 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
         p.ksplit = 1;
         const dim3 sgrid((unsigned)(((a->out_w + ST_TW - 1) / ST_TW) * ((a->out_h + ST_TH - 1) / ST_TH) * a->batch));
         if (N == 64) hipLaunchKernelGGL((stem_conv_kernel<64>), sgrid, dim3(256), 0, s, p);
-        else hipLaunchKernelGGL((stem_conv_kernel<32>), sgrid, dim3(256), 0, s, p);
+        else if (N == 32) hipLaunchKernelGGL((stem_conv_kernel<32>), sgrid, dim3(256), 0, s, p);
+        else if (N == 16) hipLaunchKernelGGL((stem_conv_kernel<16>), sgrid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((stem_conv_kernel<8>), sgrid, dim3(256), 0, s, p);
         return check_launch("pu_conv_igemm (stem)");
     }
     if (conv1x1_small_ok(a)) {
@@ -1466,7 +1469,7 @@ extern "C" int pu_split_weight6(const float* packed, void* out, int n, int k_pad
 extern "C" size_t pu_conv_igemm_workspace_bytes(const pu_conv_args* a) {
     if (!a || a->batch <= 0 || a->out_h <= 0 || a->out_w <= 0 || a->n <= 0 || a->k_pad <= 0) return 0;
     const long long M = (long long)a->batch * a->out_h * a->out_w;
-    if (small_conv_ok(a) || stem_conv_ok(a) || conv1x1_small_ok(a)) return 0;
+    if (small_conv_ok(a) || stem_conv_ok(a) || conv1x1_small_ok(a) || smallx6_ok(a, vec_epilogue(a))) return 0;
     if (wino_ok(a, vec_epilogue(a))) return wino_workspace_bytes(a);
     int bm, bn, ks, tp;
     plan_tiles(a, M, &bm, &bn, &ks, &tp);
@@ -1494,8 +1497,8 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         if (ksplit) *ksplit = 1;
         return PU_OK;
     }
-    if (smallx6_ok(a, vec_epilogue(a))) {   // reported as mode 7 ("x6s"), 16 x 32 pixels x n
-        *bm = 512;
+    if (smallx6_ok(a, vec_epilogue(a))) {   // reported as mode 7 ("x6s"), 16 x 32 pixels x n (stride 2: 4 x 32)
+        *bm = a->stride == 2 ? 128 : 512;
         *bn = a->n;
         *mode = 7;
         if (ksplit) *ksplit = 1;

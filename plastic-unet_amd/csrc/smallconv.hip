@@ -28,7 +28,7 @@
 
 namespace pu {
 
-constexpr int SX_TW = 32, SX_HW = SX_TW + 2;         // output tile width, halo width
+constexpr int SX_TW = 32;                            // output tile width
 // output tile height: 16 rows for C = 8 (29 KB of split halo images, 5 blocks per CU); 8 rows for
 // C = 16, whose 16-row images (59 KB) held the kernel to 2 blocks per CU - at 33 KB it runs 4
 // (PU_SX16_TH=16 restores the 16-row tile for A/B runs)
@@ -38,8 +38,11 @@ constexpr int SX_TW = 32, SX_HW = SX_TW + 2;         // output tile width, halo 
 #ifndef PU_SX_PAIR
 #define PU_SX_PAIR 1
 #endif
-template <int C> constexpr int sx_th() { return C == 8 ? 16 : PU_SX16_TH; }
-template <int C> constexpr int sx_hp() { return (sx_th<C>() + 2) * SX_HW; }   // halo pixels (612 / 340)
+// stride 2 (S = 2: the 3x3 / s2 data gradient of the ConvTranspose2d of unet_p_res.py:207-217 at
+// the 8-channel level): 4-row tiles, the halo spans (2 * 4 + 1) x (2 * 32 + 1) input pixels (28 KB)
+template <int C, int S = 1> constexpr int sx_th() { return S == 2 ? 4 : C == 8 ? 16 : PU_SX16_TH; }
+template <int S> constexpr int sx_hw() { return (SX_TW - 1) * S + 3; }                 // halo width 34 / 65
+template <int C, int S = 1> constexpr int sx_hp() { return ((sx_th<C, S>() - 1) * S + 3) * sx_hw<S>(); }   // halo pixels
 
 typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
 typedef float f32x4s __attribute__((ext_vector_type(4)));
@@ -50,11 +53,11 @@ typedef float f32x4s __attribute__((ext_vector_type(4)));
 // One block per tile.  LDS allows 4-5 blocks per CU (29 / 33 KB): waves_per_eu(4) lets the compiler
 // use 128 registers instead of squeezing into 64 with the accumulators parked in AGPRs (320 accvgpr
 // moves per wave at C = 8)
-template <int C, int N>
+template <int C, int N, int S = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() == 16 && C == 16 ? 2 : 4))) void smallconv_x6_kernel(const IgemmParams p) {
 #pragma clang fp contract(off)
-    constexpr int SX_TH = sx_th<C>(), SX_HP = sx_hp<C>();
-    constexpr bool PAIR = PU_SX_PAIR && N == 8;     // two output rows per group (header)
+    constexpr int SX_TH = sx_th<C, S>(), SX_HP = sx_hp<C, S>(), SX_HW = sx_hw<S>();
+    constexpr bool PAIR = PU_SX_PAIR && N == 8 && S == 1;   // two output rows per group (header)
     constexpr int RPW = SX_TH / 4;                  // output rows per wave
     constexpr int GR = PAIR ? RPW : 2 * RPW;        // groups (16 pixels x 1 or 2 rows) per wave
     constexpr int HALVES = C / 8;                   // 8-channel LDS images per plane
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
     blk /= tiles_w;
     const int tyi = blk % tiles_h;
     const int b = blk / tiles_h;
-    const int y0 = tyi * SX_TH - 1, x0 = txi * SX_TW - 1;   // halo origin (pad 1)
+    const int y0 = tyi * SX_TH * S - p.pad, x0 = txi * SX_TW * S - p.pad;   // halo origin
     const long long imgpix = (long long)b * p.Hi * p.Wi;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
 #pragma unroll
         for (int t = 0; t < GR; ++t) {
             const int row = RPW * wave + (PAIR ? 2 * (t >> 1) : t >> 1), col = (t & 1) * 16 + j;
-            const int hp = (row + r) * SX_HW + col + sx;
+            const int hp = (row * S + r) * SX_HW + col * S + sx;
             // k past 9C (tap >= 9) reads tap 0's window: finite values against zero weight planes
             bf16x8s xb[3];
 #pragma unroll
@@ -187,19 +190,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
 }
 
 // C in {8, 16} from one source or two 8-channel-aligned ones, N in {8, 16}, 3x3 / s1 / p1 same
-// size, tap-major fp32 weight rows (k_pad = 9C rounded to 16), float4 epilogue, no ConvT shuffle
+// size - or C = 8 from one source at stride 2, pad 0 / 1 (the ConvT data gradient) - tap-major fp32
+// weight rows (k_pad = 9C rounded to 16), float4 epilogue, no ConvT shuffle
 bool smallx6_ok(const pu_conv_args* a, bool vec_epi) {
     const int C = a->c0 + a->c1;
+    const bool s1 = a->stride == 1 && a->pad == 1 && a->in_h == a->out_h && a->in_w == a->out_w;
+    const bool s2 = a->stride == 2 && (a->pad == 0 || a->pad == 1) && C == 8 && a->c1 == 0 &&
+                    2 * (a->out_h - 1) + 3 - a->pad <= a->in_h + a->pad && 2 * (a->out_w - 1) + 3 - a->pad <= a->in_w + a->pad;
     return !(a->flags & PU_CONV_NO_SMALLX6) && a->weight6 && (C == 8 || C == 16) && (a->n == 8 || a->n == 16) && a->c0 % 8 == 0 &&
-           a->c1 % 8 == 0 && a->kh == 3 && a->kw == 3 && a->stride == 1 && a->pad == 1 &&
-           a->in_h == a->out_h && a->in_w == a->out_w && !(a->flags & PU_EPI_SHUFFLE2) && vec_epi &&
+           a->c1 % 8 == 0 && a->kh == 3 && a->kw == 3 && (s1 || s2) && !(a->flags & PU_EPI_SHUFFLE2) && vec_epi &&
            (a->cgroup == 0 || a->cgroup >= C) && a->k_pad == (9 * C + 15) / 16 * 16;
 }
 
 int smallx6_launch(const pu_conv_args* a, const IgemmParams& p, hipStream_t s) {
     const int C = a->c0 + a->c1;
-    const int th = C == 8 ? sx_th<8>() : sx_th<16>();
+    const int th = a->stride == 2 ? sx_th<8, 2>() : C == 8 ? sx_th<8>() : sx_th<16>();
     const dim3 grid((unsigned)(((a->out_w + SX_TW - 1) / SX_TW) * ((a->out_h + th - 1) / th) * a->batch));
+    if (a->stride == 2) {
+        if (a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 8, 2>), grid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((smallconv_x6_kernel<8, 16, 2>), grid, dim3(256), 0, s, p);
+        return check_launch("pu_conv_igemm (small-channel x6, stride 2)");
+    }
     if (C == 8 && a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 8>), grid, dim3(256), 0, s, p);
     else if (C == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 16>), grid, dim3(256), 0, s, p);
     else if (a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<16, 8>), grid, dim3(256), 0, s, p);

@@ -42,7 +42,8 @@ def assert_close(got, ref, rtol=1e-4, atol_rel=1e-5):
 
 CONV_CASES = [
     # B, H, W, c0, c1, cout
-    (2, 16, 16, 1, 0, 8),       # stem: scalar loader
+    (2, 16, 16, 1, 0, 8),       # single-channel stem kernel (N = 8)
+    (2, 37, 70, 1, 0, 16),      # single-channel stem kernel (N = 16): partial 16 x 64 tiles
     (2, 40, 70, 1, 0, 64),      # single-channel stem kernel (N = 64): partial 16 x 64 tiles
     (1, 17, 33, 1, 0, 32),      # single-channel stem kernel (N = 32), odd sizes
     (2, 12, 20, 8, 0, 16),      # vec4 loader, non-square

@@ -38,7 +38,10 @@ def assert_close(got, ref, rtol=1e-4, atol_rel=1e-5):
 
 
 @pytest.mark.parametrize("B,h,cin,cout,crop", [(2, 6, 16, 8, 1), (1, 12, 32, 16, 0), (2, 5, 64, 32, 1),
-                                               (1, 3, 8, 4, 0)])
+                                               (1, 3, 8, 4, 0),
+                                               # 8-channel dU: the stride-2 small-channel MFMA dgrad
+                                               (2, 16, 8, 8, 1), (1, 20, 16, 8, 0), (2, 37, 16, 8, 1),
+                                               (1, 5, 8, 8, 0)])
 def test_convT3x3_s2_crop(B, h, cin, cout, crop):
     """ConvTranspose2d(3, s=2, p=0) + the F.pad crop of unet_p_res.py:214-217: fwd, dgrad, wgrad, bias."""
     g = torch.Generator().manual_seed(h * 100 + cin + crop)
