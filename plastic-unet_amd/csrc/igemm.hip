@@ -1498,7 +1498,7 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         return PU_OK;
     }
     if (smallx6_ok(a, vec_epilogue(a))) {   // reported as mode 7 ("x6s"), 16 x 32 pixels x n (stride 2: 4 x 32)
-        *bm = a->stride == 2 ? 128 : 512;
+        *bm = a->stride == 2 ? 128 : a->kh == 2 ? 256 : 512;
         *bn = a->n;
         *mode = 7;
         if (ksplit) *ksplit = 1;

@@ -40,28 +40,31 @@ constexpr int SX_TW = 32;                            // output tile width
 #endif
 // stride 2 (S = 2: the 3x3 / s2 data gradient of the ConvTranspose2d of unet_p_res.py:207-217 at
 // the 8-channel level): 4-row tiles, the halo spans (2 * 4 + 1) x (2 * 32 + 1) input pixels (28 KB)
+// KT = 2 (2 x 2 taps, N = 32: the ConvTranspose2d 3x3 / s2 forward of the 16-channel level as its
+// 2 x 2 sub-pixel conv, unet_p_res.py:207-217, stored through the SHUFFLE2 epilogue)
 template <int C, int S = 1> constexpr int sx_th() { return S == 2 ? 4 : C == 8 ? 16 : PU_SX16_TH; }
-template <int S> constexpr int sx_hw() { return (SX_TW - 1) * S + 3; }                 // halo width 34 / 65
-template <int C, int S = 1> constexpr int sx_hp() { return ((sx_th<C, S>() - 1) * S + 3) * sx_hw<S>(); }   // halo pixels
+template <int S, int KT = 3> constexpr int sx_hw() { return (SX_TW - 1) * S + KT; }       // halo width 34 / 65 / 33
+template <int C, int S = 1, int KT = 3> constexpr int sx_hp() {                          // halo pixels
+    return ((sx_th<C, S>() - 1) * S + KT) * sx_hw<S, KT>();
+}
 
 typedef __bf16 bf16x8s __attribute__((ext_vector_type(8)));
 typedef float f32x4s __attribute__((ext_vector_type(4)));
 
-// LDS allows 4-5 blocks per CU (29 / 33 KB): waves_per_eu(4) lets the compiler use 128 registers
-// instead of squeezing into 64 with the accumulators parked in AGPRs (320 accvgpr moves per wave at
-// C = 8)
 // One block per tile.  LDS allows 4-5 blocks per CU (29 / 33 KB): waves_per_eu(4) lets the compiler
 // use 128 registers instead of squeezing into 64 with the accumulators parked in AGPRs (320 accvgpr
 // moves per wave at C = 8)
-template <int C, int N, int S = 1>
+template <int C, int N, int S = 1, int KT = 3>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() == 16 && C == 16 ? 2 : 4))) void smallconv_x6_kernel(const IgemmParams p) {
 #pragma clang fp contract(off)
-    constexpr int SX_TH = sx_th<C, S>(), SX_HP = sx_hp<C, S>(), SX_HW = sx_hw<S>();
-    constexpr bool PAIR = PU_SX_PAIR && N == 8 && S == 1;   // two output rows per group (header)
+    constexpr int SX_TH = sx_th<C, S>(), SX_HP = sx_hp<C, S, KT>(), SX_HW = sx_hw<S, KT>();
+    constexpr bool PAIR = PU_SX_PAIR && N == 8 && S == 1 && KT == 3;   // two output rows per group (header)
+    constexpr int NB = (N + 15) / 16;               // 16-row blocks of A (N = 32: two)
+    constexpr int TAPS = KT * KT;
     constexpr int RPW = SX_TH / 4;                  // output rows per wave
     constexpr int GR = PAIR ? RPW : 2 * RPW;        // groups (16 pixels x 1 or 2 rows) per wave
     constexpr int HALVES = C / 8;                   // 8-channel LDS images per plane
-    constexpr int KS = PAIR ? 12 * C / 32 : (9 * C + 31) / 32;   // 32-wide k steps
+    constexpr int KS = PAIR ? 12 * C / 32 : (TAPS * C + 31) / 32;   // 32-wide k steps
     static_assert(!PAIR || RPW % 2 == 0, "row pairs need an even number of rows per wave");
     // [plane][half][pixel][8 channels] bf16
     __shared__ __attribute__((aligned(16))) __bf16 img[3 * HALVES * SX_HP * 8];
@@ -80,9 +83,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
 
     // ---- weights: lane (row n = lane & 15, k-group g = lane >> 4) holds k = 32s + 8g .. +7 of
     // every step s as hi/mid/lo planes (rows >= N and k >= 9C are zero)
-    bf16x8s wa[KS][3];
-    {
-        const int n = lane & 15, g = lane >> 4;
+    bf16x8s wa[NB][KS][3];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+        const int n = 16 * nb + (lane & 15), g = lane >> 4;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             f32x4s lo = {0.f, 0.f, 0.f, 0.f}, hi = {0.f, 0.f, 0.f, 0.f};
@@ -93,11 +97,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
                     lo = *reinterpret_cast<const f32x4s*>(p.wt + (n & 7) * p.k_pad + wk);
                     hi = *reinterpret_cast<const f32x4s*>(p.wt + (n & 7) * p.k_pad + wk + 4);
                 }
-            } else if (n < N && k < 9 * C) {   // 9C is a multiple of 8: the 8 k are all real or all padding
+            } else if (n < N && k < TAPS * C) {   // TAPS*C is a multiple of 8: the 8 k are all real or all padding
                 lo = *reinterpret_cast<const f32x4s*>(p.wt + n * p.k_pad + k);
                 hi = *reinterpret_cast<const f32x4s*>(p.wt + n * p.k_pad + k + 4);
             }
-            split3_pairs(lo, hi, wa[s][0], wa[s][1], wa[s][2]);
+            split3_pairs(lo, hi, wa[nb][s][0], wa[nb][s][1], wa[nb][s][2]);
         }
     }
 
@@ -147,32 +151,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
 
     // ---- MFMAs: wave w owns output rows RPW w .. RPW w + RPW-1, each 2 groups of 16 pixels
     const int j = lane & 15, g = lane >> 4;
-    f32x4s acc[GR];
+    f32x4s acc[GR][NB];
 #pragma unroll
-    for (int t = 0; t < GR; ++t) acc[t] = f32x4s{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < GR; ++t)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[t][nb] = f32x4s{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
         const int k = 32 * s + 8 * g;               // this lane's 8 k: one (super-)tap, 8 channels
         const int tap = k / C, c8 = (k % C) / 8;
-        const bool live = PAIR || tap < 9;
-        const int r = live ? tap / 3 : 0, sx = live ? tap % 3 : 0;
+        const bool live = PAIR || tap < TAPS;
+        const int r = live ? tap / KT : 0, sx = live ? tap % KT : 0;
 #pragma unroll
         for (int t = 0; t < GR; ++t) {
             const int row = RPW * wave + (PAIR ? 2 * (t >> 1) : t >> 1), col = (t & 1) * 16 + j;
             const int hp = (row * S + r) * SX_HW + col * S + sx;
-            // k past 9C (tap >= 9) reads tap 0's window: finite values against zero weight planes
+            // k past TAPS*C reads tap 0's window: finite values against zero weight planes
             bf16x8s xb[3];
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
                 xb[pl] = *reinterpret_cast<const bf16x8s*>(img + ((pl * HALVES + c8) * SX_HP + hp) * 8);
-            f32x4s c = acc[t];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][1], xb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][2], xb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][0], xb[2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][1], xb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][0], xb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[s][0], xb[0], c, 0, 0, 0);
-            acc[t] = c;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) {
+                f32x4s c = acc[t][nb];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb][s][1], xb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb][s][2], xb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb][s][0], xb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb][s][1], xb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb][s][0], xb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[nb][s][0], xb[0], c, 0, 0, 0);
+                acc[t][nb] = c;
+            }
         }
     }
 
@@ -185,14 +194,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sx_th<C>() 
         const int ox = txi * SX_TW + (t & 1) * 16 + j;
         if (oy >= p.Ho || ox >= p.Wo) continue;
         const int m = (b * p.Ho + oy) * p.Wo + ox;
-        epi_store4(p, epi_row(p, m), PAIR ? 4 * (g & 1) : 4 * g, acc[t]);
+        const EpiRow er = epi_row(p, m);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) epi_store4(p, er, 16 * nb + (PAIR ? 4 * (g & 1) : 4 * g), acc[t][nb]);
     }
 }
 
 // C in {8, 16} from one source or two 8-channel-aligned ones, N in {8, 16}, 3x3 / s1 / p1 same
 // size - or C = 8 from one source at stride 2, pad 0 / 1 (the ConvT data gradient) - tap-major fp32
-// weight rows (k_pad = 9C rounded to 16), float4 epilogue, no ConvT shuffle
+// weight rows (k_pad = 9C rounded to 16), float4 epilogue, no ConvT shuffle; or the ConvT forward's
+// 2 x 2 / p1 sub-pixel conv of 16 channels into N = 32 (4 x 8 channels, SHUFFLE2)
+static bool smallx6_convt_ok(const pu_conv_args* a, bool vec_epi) {
+    return !(a->flags & PU_CONV_NO_SMALLX6) && a->weight6 && a->c0 == 16 && a->c1 == 0 && a->n == 32 &&
+           a->kh == 2 && a->kw == 2 && a->stride == 1 && a->pad == 1 && a->out_h == a->in_h + 1 &&
+           a->out_w == a->in_w + 1 && (a->flags & PU_EPI_SHUFFLE2) && vec_epi && a->cgroup == 0 && a->k_pad == 64;
+}
+
 bool smallx6_ok(const pu_conv_args* a, bool vec_epi) {
+    if (smallx6_convt_ok(a, vec_epi)) return true;
     const int C = a->c0 + a->c1;
     const bool s1 = a->stride == 1 && a->pad == 1 && a->in_h == a->out_h && a->in_w == a->out_w;
     const bool s2 = a->stride == 2 && (a->pad == 0 || a->pad == 1) && C == 8 && a->c1 == 0 &&
@@ -206,6 +225,10 @@ int smallx6_launch(const pu_conv_args* a, const IgemmParams& p, hipStream_t s) {
     const int C = a->c0 + a->c1;
     const int th = a->stride == 2 ? sx_th<8, 2>() : C == 8 ? sx_th<8>() : sx_th<16>();
     const dim3 grid((unsigned)(((a->out_w + SX_TW - 1) / SX_TW) * ((a->out_h + th - 1) / th) * a->batch));
+    if (a->kh == 2) {
+        hipLaunchKernelGGL((smallconv_x6_kernel<16, 32, 1, 2>), grid, dim3(256), 0, s, p);
+        return check_launch("pu_conv_igemm (small-channel x6, ConvT 2x2 sub-pixel)");
+    }
     if (a->stride == 2) {
         if (a->n == 8) hipLaunchKernelGGL((smallconv_x6_kernel<8, 8, 2>), grid, dim3(256), 0, s, p);
         else hipLaunchKernelGGL((smallconv_x6_kernel<8, 16, 2>), grid, dim3(256), 0, s, p);

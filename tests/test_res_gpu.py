@@ -41,7 +41,10 @@ def assert_close(got, ref, rtol=1e-4, atol_rel=1e-5):
                                                (1, 3, 8, 4, 0),
                                                # 8-channel dU: the stride-2 small-channel MFMA dgrad
                                                (2, 16, 8, 8, 1), (1, 20, 16, 8, 0), (2, 37, 16, 8, 1),
-                                               (1, 5, 8, 8, 0)])
+                                               (1, 5, 8, 8, 0),
+                                               # 16 -> 8 channels: the ConvT forward on the
+                                               # small-channel MFMA kernel (2 x 2 sub-pixel conv)
+                                               (2, 19, 16, 8, 1), (1, 40, 16, 8, 0)])
 def test_convT3x3_s2_crop(B, h, cin, cout, crop):
     """ConvTranspose2d(3, s=2, p=0) + the F.pad crop of unet_p_res.py:214-217: fwd, dgrad, wgrad, bias."""
     g = torch.Generator().manual_seed(h * 100 + cin + crop)
