@@ -1782,7 +1782,7 @@ struct WgradPlan {
 };
 
 static bool stem_wgrad_ok(const pu_wgrad_args* a) {
-    return a->c0 == 1 && a->c1 == 0 && (a->n == 32 || a->n == 64) && a->kh == 3 && a->kw == 3 && a->stride == 1 &&
+    return a->c0 == 1 && a->c1 == 0 && (a->n == 8 || a->n == 16 || a->n == 32 || a->n == 64) && a->kh == 3 && a->kw == 3 && a->stride == 1 &&
            a->pad == 1 && a->in_h == a->out_h && a->in_w == a->out_w && a->bias_mode == 1 &&
            ((uintptr_t)a->rows & 15) == 0;
 }
@@ -2583,7 +2583,9 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
     p.batch = a->batch; p.tiles_w = pl.tiles_w; p.tiles_h = pl.tiles_h;
     if (pl.stem && (phase & 1)) {
         if (a->n == 64) hipLaunchKernelGGL(wgrad_stem_kernel<64>, dim3(pl.splits), dim3(256), 0, s, p);
-        else hipLaunchKernelGGL(wgrad_stem_kernel<32>, dim3(pl.splits), dim3(256), 0, s, p);
+        else if (a->n == 32) hipLaunchKernelGGL(wgrad_stem_kernel<32>, dim3(pl.splits), dim3(256), 0, s, p);
+        else if (a->n == 16) hipLaunchKernelGGL(wgrad_stem_kernel<16>, dim3(pl.splits), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL(wgrad_stem_kernel<8>, dim3(pl.splits), dim3(256), 0, s, p);
         st = check_launch("pu_wgrad (stem)");
         if (st != PU_OK) return st;
         phase &= ~1;

@@ -173,6 +173,8 @@ def test_wgrad_dispatch_plan_takes_winograd_on_c2_layers():
     assert K.wgrad_kind(batch=4, hw=(101, 101), n=64, c0=64) != 5       # odd grid
     assert K.wgrad_kind(batch=4, hw=(64, 64), n=32, c0=32) != 5         # 32-channel layer
     assert K.wgrad_kind(batch=4, hw=(64, 64), n=8, c0=8) == 2            # small-channel direct
+    for n in (8, 16, 32, 64):                                            # single-channel stem
+        assert K.wgrad_kind(batch=4, hw=(64, 64), n=n, c0=1) == 4, n
     # C4's CoordConv 1x1 (4 -> 8 channels at 256^2) takes the pointwise kernel; a 64-channel 1x1 not
     assert K.wgrad_kind(batch=32, hw=(256, 256), n=8, c0=4, k=1) == 6
     assert K.wgrad_kind(batch=2, hw=(24, 40), n=16, c0=3, k=1) == 6
