@@ -205,7 +205,7 @@ __device__ __forceinline__ f32x4 fh_ld4<__bf16>(const __bf16* p) {
     return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
 
-template <typename T, int L, int TPW>
+template <typename T, int L, int TPW, int R = FH_R>
 __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ wo,
                                                                const float* __restrict__ bo, int C,
                                                                const float* __restrict__ H, const float* __restrict__ w,
@@ -213,12 +213,13 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
                                                                const float* __restrict__ eta_p, float* __restrict__ X,
                                                                float* __restrict__ Y, float* __restrict__ Hn, int N,
                                                                FastDiv dN, int kc, int rule) {
+    constexpr int RT = (R + 15) / 16;         // 16-row MFMA tiles of the block's rows
     extern __shared__ float fh_lds[];
-    float* xs = fh_lds;                       // [FH_R + 1][N]: own rows, then row 0
-    float* ws = xs + (FH_R + 1) * N;          // [kc][N]
+    float* xs = fh_lds;                       // [R + 1][N]: own rows, then row 0
+    float* ws = xs + (R + 1) * N;             // [kc][N]
     float* y0s = ws + kc * N;                 // [N]
     const int b = blockIdx.y;
-    const int i0 = blockIdx.x * FH_R;
+    const int i0 = blockIdx.x * R;
     const int tid = threadIdx.x;
     const bool fuse = Hn != nullptr;
     const long long nn = (long long)N * N;
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
         const float bias = bo ? bo[0] : 0.f;
         const int lane = tid % L;
         constexpr int PPP = FH_NT / L;          // pixels per pass
-        const int npix = (fuse ? FH_R + 1 : FH_R) * N;
+        const int npix = (fuse ? R + 1 : R) * N;
         auto reduce_store = [&](int q0, float (&s)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
         auto pixel = [&](int q) -> const T* {
             q = min(q, npix - 1);
             const int r = (int)fdiv((unsigned)q, dN), k = q - r * N;
-            return fb + ((long long)(r < FH_R ? i0 + r : 0) * N + k) * C;
+            return fb + ((long long)(r < R ? i0 + r : 0) * N + k) * C;
         };
         for (int q0 = tid / L; q0 < npix; q0 += U * PPP) {
             const T* px[U];
@@ -269,20 +270,22 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     }
     __syncthreads();
     // X rows of this block -> global (coalesced)
-    for (int e = tid; e < FH_R * N; e += FH_NT) X[(long long)b * nn + (long long)i0 * N + e] = xs[e];
+    for (int e = tid; e < R * N; e += FH_NT) X[(long long)b * nn + (long long)i0 * N + e] = xs[e];
     if (PU_FH_ABL == 1) return;
 
     // the trace update's first float4 of H (rows i0.., L2-resident after the Weff build), in
     // flight during the GEMM
     f32x4 hpre = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (fuse && tid < FH_R * N / 4) hpre = reinterpret_cast<const f32x4*>(Hb + (long long)i0 * N)[tid];
+    if (fuse && tid < R * N / 4) hpre = reinterpret_cast<const f32x4*>(Hb + (long long)i0 * N)[tid];
 
     // ---- 2. GEMM
     const int wave = tid >> 6, l = tid & 63;
     const int tiles = N / 16;
-    f32x4 acc[TPW];
+    f32x4 acc[TPW][RT];
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[t][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
     float acc0 = 0.f;                                  // y0 chain of column tid (tid < N)
     for (int k0 = 0; k0 < N; k0 += kc) {
         {
@@ -316,19 +319,28 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
             const int tile = wave + FH_WAVES * t;
             if (tile < tiles) {
                 const float* wcol = ws + (l >> 4) * N + tile * 16 + (l & 15);
-                const float* xrow = xs + (l & 15) * N + k0 + (l >> 4);
+                const float* xrow = xs + (l & 15) * N + k0 + (l >> 4);   // row tile rt: + 16 rt N
                 // operands of 4 k-steps read before their MFMAs (kc % 16 == 0 or kc = 4 .. 12: see
-                // fused_head_chunk - the tail loop takes the rest)
+                // fused_head_chunk - the tail loop takes the rest); each W fragment feeds RT tiles
                 int kk = 0;
                 for (; kk + 16 <= kc; kk += 16) {
-                    float xa[4], wb[4];
+                    float xa[RT][4], wb[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) { xa[j] = xrow[kk + 4 * j]; wb[j] = wcol[(kk + 4 * j) * N]; }
+                    for (int j = 0; j < 4; ++j) {
+                        wb[j] = wcol[(kk + 4 * j) * N];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[j], wb[j], acc[t], 0, 0, 0);
+                        for (int rt = 0; rt < RT; ++rt) xa[rt][j] = xrow[16 * rt * N + kk + 4 * j];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt)
+                            acc[t][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[rt][j], wb[j], acc[t][rt], 0, 0, 0);
                 }
                 for (; kk < kc; kk += 4)
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xrow[kk], wcol[kk * N], acc[t], 0, 0, 0);
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt)
+                        acc[t][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xrow[16 * rt * N + kk], wcol[kk * N], acc[t][rt], 0, 0, 0);
             }
         }
         if (fuse && tid < N && PU_FH_ABL != 2) {
@@ -338,11 +350,11 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
             for (; kk + 8 <= kc; kk += 8) {
                 float xa[8], wb[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) { xa[j] = xs[FH_R * N + k0 + kk + j]; wb[j] = ws[(kk + j) * N + tid]; }
+                for (int j = 0; j < 8; ++j) { xa[j] = xs[R * N + k0 + kk + j]; wb[j] = ws[(kk + j) * N + tid]; }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) s0 = fmaf(xa[j], wb[j], s0);
             }
-            for (; kk < kc; ++kk) s0 = fmaf(xs[FH_R * N + k0 + kk], ws[kk * N + tid], s0);
+            for (; kk < kc; ++kk) s0 = fmaf(xs[R * N + k0 + kk], ws[kk * N + tid], s0);
             acc0 = s0;
         }
         __syncthreads();
@@ -355,11 +367,14 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
         const int tile = wave + FH_WAVES * t;
         if (tile < tiles) {
             const int j = tile * 16 + (l & 15);
-            if (4 * (l >> 4) < FH_R) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int gi = i0 + 4 * (l >> 4) + r;
-                    Y[((long long)b * N + gi) * N + j] = 1.f / (1.f + expf(-acc[t][r]));
+            for (int rt = 0; rt < RT; ++rt) {
+                if (16 * rt + 4 * (l >> 4) < R) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int gi = i0 + 16 * rt + 4 * (l >> 4) + r;
+                        Y[((long long)b * N + gi) * N + j] = 1.f / (1.f + expf(-acc[t][rt][r]));
+                    }
                 }
             }
         }
@@ -371,13 +386,13 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
     // ---- 4. trace update of rows k = i0 .. i0+15
     const float eta = eta_p[0];
     const float one_m_eta = 1.f - eta;
-    // rows i0 .. i0+15 of H / H' are contiguous: float4 over the block's FH_R * N elements
+    // rows i0 .. i0+R-1 of H / H' are contiguous: float4 over the block's R * N elements
     const f32x4* Hr = reinterpret_cast<const f32x4*>(Hb + (long long)i0 * N);
     f32x4* Hnr = reinterpret_cast<f32x4*>(Hn + (long long)b * nn + (long long)i0 * N);
-    for (int e4 = tid; e4 < FH_R * N / 4; e4 += FH_NT) {
+    for (int e4 = tid; e4 < R * N / 4; e4 += FH_NT) {
         const f32x4 h = e4 == tid ? hpre : Hr[e4];
         const int kk = (int)fdiv((unsigned)(4 * e4), dN), j = 4 * e4 - kk * N;
-        const float x0 = xs[FH_R * N + i0 + kk];
+        const float x0 = xs[R * N + i0 + kk];
         f32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = trace_rule(h[e], x0, y0s[j + e], eta, one_m_eta, rule);
@@ -845,16 +860,25 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
         return check_launch("pu_plastic_head_fwd");
     }
     const int kc = fused_head_chunk(N);                           // Weff rows per LDS chunk
-    size_t lds = ((size_t)(FH_R + 1) * N + (size_t)kc * N + N) * sizeof(float);
+    // rows per block: every block re-forms the whole W_eff = w + alpha (.) H of its slot, so at
+    // nbf >= 256 (C4 / C5) 32-row blocks halve that work and feed each W fragment to two MFMA row
+    // tiles (the LDS of 16-row blocks already held them to one block per CU there)
+    const int R = (N >= 256 && N % 32 == 0 && ((size_t)(32 + 1) * N + (size_t)kc * N + N) * sizeof(float) <= 160 * 1024) ? 32 : FH_R;
+    size_t lds = ((size_t)(R + 1) * N + (size_t)kc * N + N) * sizeof(float);
     if (lds < (size_t)PU_FH_LDS_MIN) lds = PU_FH_LDS_MIN;
-    const dim3 grid(N / FH_R, a->batch);
+    const dim3 grid(N / R, a->batch);
     const FastDiv dN = make_fastdiv(N);
     hipStream_t s = as_stream(stream);
     const int tpw = (N / 16 + FH_WAVES - 1) / FH_WAVES;           // column tiles per wave
-#define PU_FH2(T_, L_, W_)                                                                                     \
-    hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat,     \
+#define PU_FH3(T_, L_, W_, R_)                                                                                 \
+    hipLaunchKernelGGL((head_fused_fwd_kernel<T_, L_, W_, R_>), grid, dim3(FH_NT), lds, s, (const T_*)a->feat, \
                        a->out_w, a->out_b, C, a->hebb, a->w, a->alpha, a->eta, a->x, a->y, a->hebb_out, N, dN, kc, \
                        a->rule)
+#define PU_FH2(T_, L_, W_)                                                                                     \
+    do {                                                                                                    \
+        if (R == 32) PU_FH3(T_, L_, W_, 32);                                                                \
+        else PU_FH3(T_, L_, W_, FH_R);                                                                      \
+    } while (0)
 #define PU_FH(T_, L_)                                                                                       \
     do {                                                                                                    \
         if (tpw <= 1) PU_FH2(T_, L_, 1);                                                                    \
@@ -873,6 +897,7 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
 #undef PU_FH_L
 #undef PU_FH
 #undef PU_FH2
+#undef PU_FH3
     return check_launch("pu_plastic_head_fwd");
 }
 

@@ -389,6 +389,9 @@ def test_fused_head_trace_equals_two_launch_path(B, N, rule):
                                       # power of two (chunk 72 / 64 / 40 / 32 rows)
                                       (2, 144, 64, torch.float32), (1, 192, 16, torch.float32),
                                       (1, 320, 8, torch.float32), (1, 384, 64, torch.float32),
+                                      # 32-row blocks (N >= 256, N % 32 == 0) and the 16-row
+                                      # fallback at N = 272
+                                      (2, 256, 16, torch.bfloat16), (1, 272, 8, torch.float32),
                                       # the pipelined single-chunk path (C == 4 L) at every L
                                       (4, 64, 4, torch.float32), (2, 112, 32, torch.bfloat16)])
 def test_fused_head_equals_outconv_then_head(rule, B, N, C, dt):
