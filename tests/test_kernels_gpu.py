@@ -288,6 +288,29 @@ def test_trace_sequence_golden(rule):
         assert_close(H[0], torch.from_numpy(g["H"][k]))
 
 
+@pytest.mark.parametrize("B,N", [(8, 512), (32, 256), (2, 128)])
+def test_plastic_bwd_against_fp64(B, N):
+    """pu_plastic_bwd on both tile paths (64-tiles on v_mfma_f32_16x16x4_f32 when the grid has
+    >= 512 blocks: 8 x 512^2, 32 x 256^2; 32-tiles on the VALU otherwise) against the fp64
+    gradients dX = G Weff^T, dw = sum_b X_b^T G_b, dalpha = sum_b (X_b^T G_b) . H_b with
+    G = dY (1 - Y) Y."""
+    g = torch.Generator().manual_seed(B + N)
+    X = rnd(B, N, N, g=g, scale=2.0)
+    H = rnd(B, N, N, g=g, scale=0.2)
+    w = rnd(N, N, g=g, scale=0.05)
+    al = torch.rand(N, N, generator=g) * 0.05
+    Y = torch.rand(B, N, N, generator=g)
+    dY = rnd(B, N, N, g=g)
+    dx, dw, da = K.plastic_bwd(X.to(DEV), H.to(DEV), w.to(DEV), al.to(DEV), Y.to(DEV), dY.to(DEV))
+    Gd = dY.double() * (1 - Y.double()) * Y.double()
+    weff = w.double()[None] + al.double()[None] * H.double()
+    T = torch.einsum("bik,bij->bkj", X.double(), Gd)
+    ref_dx = torch.einsum("bij,bkj->bik", Gd, weff)
+    for got, ref in ((dx, ref_dx), (dw, T.sum(0)), (da, (T * H.double()).sum(0))):
+        got = got.cpu().double()
+        assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, (got - ref).abs().max()
+
+
 def test_plastic_head_batched_slots_match_oracle():
     g = torch.Generator().manual_seed(9)
     B, N = 32, 128
