@@ -597,7 +597,6 @@ __global__ __launch_bounds__(256) void head_dx_kernel(const float* __restrict__ 
     const long long off = (long long)b * N * N;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     float acc[M][M] = {};
-    f32x4 macc[4] = {};                // T = 64: the MFMA form's accumulators
     for (int j0 = 0; j0 < N; j0 += HK) {
         for (int e = threadIdx.x; e < HK * T; e += 256) {
             int jj = e % HK, rr = e / HK;
@@ -618,44 +617,17 @@ __global__ __launch_bounds__(256) void head_dx_kernel(const float* __restrict__ 
             ws[jj][rr] = v;
         }
         __syncthreads();
-        if constexpr (T == 64) {
-            // v_mfma_f32_16x16x4_f32: wave w owns rows i 16w .. 16w+15 x the 4 column tiles of k;
-            // its k-ordered fma chain equals the VALU form's (the fused head relies on the same)
-            const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-            for (int jj = 0; jj < HK; jj += 4) {
-                const float av = gs[jj + (l >> 4)][16 * w + (l & 15)];
+        for (int jj = 0; jj < HK; ++jj) {
+            float a[M], bb[M];
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    macc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ws[jj + (l >> 4)][16 * c + (l & 15)], macc[c], 0, 0, 0);
-            }
-        } else {
+            for (int q = 0; q < M; ++q) { a[q] = gs[jj][ty * M + q]; bb[q] = ws[jj][tx * M + q]; }
 #pragma unroll
-            for (int jj = 0; jj < HK; ++jj) {
-                float a[M], bb[M];
+            for (int q = 0; q < M; ++q)
 #pragma unroll
-                for (int q = 0; q < M; ++q) { a[q] = gs[jj][ty * M + q]; bb[q] = ws[jj][tx * M + q]; }
-#pragma unroll
-                for (int q = 0; q < M; ++q)
-#pragma unroll
-                    for (int r = 0; r < M; ++r) acc[q][r] = fmaf(a[q], bb[r], acc[q][r]);
-            }
+                for (int r = 0; r < M; ++r) acc[q][r] = fmaf(a[q], bb[r], acc[q][r]);
         }
         __syncthreads();
-    }
-    if constexpr (T == 64) {
-        // D lane layout: column k = 16c + (l & 15), rows i = 16w + 4 (l >> 4) + r
-        const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int gk = k0 + 16 * c + (l & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int gi = i0 + 16 * w + 4 * (l >> 4) + r;
-                if (gi < N && gk < N) dX[off + (long long)gi * N + gk] = macc[c][r];
-            }
-        }
-        return;
     }
 #pragma unroll
     for (int q = 0; q < M; ++q) {
@@ -684,7 +656,6 @@ __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ 
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const long long off = (long long)b * N * N;
     float t[M][M] = {};
-    f32x4 macc[4] = {};                // T = 64: the MFMA form's accumulators
     for (int i0 = 0; i0 < N; i0 += HK) {
         for (int e = threadIdx.x; e < HK * T; e += 256) {
             int cc = e % T, ii = e / T;
@@ -699,49 +670,20 @@ __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ 
             gs[ii][cc] = g;
         }
         __syncthreads();
-        if constexpr (T == 64) {
-            // wave w owns rows k 16w .. 16w+15 x the 4 column tiles of j (k-ordered fma chain over i)
-            const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-            for (int ii = 0; ii < HK; ii += 4) {
-                const float av = xs[ii + (l >> 4)][16 * w + (l & 15)];
+        for (int ii = 0; ii < HK; ++ii) {
+            float a[M], bb[M];
 #pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    macc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, gs[ii + (l >> 4)][16 * c + (l & 15)], macc[c], 0, 0, 0);
-            }
-        } else {
+            for (int q = 0; q < M; ++q) { a[q] = xs[ii][ty * M + q]; bb[q] = gs[ii][tx * M + q]; }
 #pragma unroll
-            for (int ii = 0; ii < HK; ++ii) {
-                float a[M], bb[M];
+            for (int q = 0; q < M; ++q)
 #pragma unroll
-                for (int q = 0; q < M; ++q) { a[q] = xs[ii][ty * M + q]; bb[q] = gs[ii][tx * M + q]; }
-#pragma unroll
-                for (int q = 0; q < M; ++q)
-#pragma unroll
-                    for (int r = 0; r < M; ++r) t[q][r] = fmaf(a[q], bb[r], t[q][r]);
-            }
+                for (int r = 0; r < M; ++r) t[q][r] = fmaf(a[q], bb[r], t[q][r]);
         }
         __syncthreads();
     }
     float* pw = partial + (long long)b * 2 * N * N;
     float* pa = pw + (long long)N * N;
-    if constexpr (T == 64) {
-        const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int gj = j0 + 16 * c + (l & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int gk = k0 + 16 * w + 4 * (l >> 4) + r;
-                if (gk < N && gj < N) {
-                    const long long o = (long long)gk * N + gj;
-                    pw[o] = macc[c][r];
-                    pa[o] = macc[c][r] * H[off + o];
-                }
-            }
-        }
-        return;
-    }
 #pragma unroll
     for (int q = 0; q < M; ++q) {
         int gk = k0 + ty * M + q;

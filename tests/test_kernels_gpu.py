@@ -290,10 +290,9 @@ def test_trace_sequence_golden(rule):
 
 @pytest.mark.parametrize("B,N", [(8, 512), (32, 256), (2, 128)])
 def test_plastic_bwd_against_fp64(B, N):
-    """pu_plastic_bwd on both tile paths (64-tiles on v_mfma_f32_16x16x4_f32 when the grid has
-    >= 512 blocks: 8 x 512^2, 32 x 256^2; 32-tiles on the VALU otherwise) against the fp64
-    gradients dX = G Weff^T, dw = sum_b X_b^T G_b, dalpha = sum_b (X_b^T G_b) . H_b with
-    G = dY (1 - Y) Y."""
+    """pu_plastic_bwd on both tile sizes (64-tiles when the grid has >= 512 blocks: 8 x 512^2,
+    32 x 256^2; 32-tiles otherwise) against the fp64 gradients dX = G Weff^T,
+    dw = sum_b X_b^T G_b, dalpha = sum_b (X_b^T G_b) . H_b with G = dY (1 - Y) Y."""
     g = torch.Generator().manual_seed(B + N)
     X = rnd(B, N, N, g=g, scale=2.0)
     H = rnd(B, N, N, g=g, scale=0.2)
