@@ -23,8 +23,11 @@ Rank 0 prints ONE JSON line.  Besides the contract fields it carries
   kernels       per-kernel-instantiation time/FLOP breakdown of one step
   oja_update    the Oja trace update's algorithmic GB/s (bs x 128^2, cache-resident) and an
                 HBM-sized sweep (8192 traces, 1 GiB per pass)
+  allreduce     the gradient exchange (N > 1): bucket count and sizes, buckets issued during the
+                backward, exposed all-reduce ms per step (HIP events, untimed pass)
   cpu_baseline  the CPU oracle (oracle/ref_cpu.py, fixture-pinned restatement of the reference)
-                in the reference's own mode (bs=1, Adam per sample) on the host cores, N=1 only
+                on the host cores, N=1 only: the reference's own mode (bs=1, Adam per sample) as
+                `value`, and the batched mode (bs B, per-slot traces) as `batched`
 """
 import argparse
 import json
@@ -53,7 +56,7 @@ def parse():
     ap.add_argument("--rule", default="oja")
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--steplr", type=float, default=1e5)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (per mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-profile", action="store_true")
     ap.add_argument("--no-oja", action="store_true", help="skip the Oja-update HBM benchmark")
@@ -101,33 +104,52 @@ def fp32_mfma_peak_tflops(kernels):
     return 256.0 * cu * clk_ghz / 1e3, cu, clk_ghz
 
 
-def cpu_baseline(args):
-    """The oracle's reference-mode training loop on the host cores: bs=1, Adam per sample."""
+def cpu_baseline(args, batch):
+    """The oracle on the host cores (SURVEY 8(d) CPU baseline), two timings of one bounded sample
+    each (args.cpu_seconds of training, after one untimed warm-up step):
+      (i)  the reference's own mode: bs=1, Adam + StepLR per sample, the trace carried sample to
+           sample (train.py:91-112) - `value`, the faithful baseline;
+      (ii) batched: the bench's per-GPU batch B with per-slot traces [B,N,N] carried step to step
+           (the batched semantics of SURVEY 8(a)), one Adam step per batch - `batched`."""
     import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
-    torch.manual_seed(0)
-    net = build_model(args, None, ref=True)
-    net.train()
-    opt = oracle.ref_adam(net.parameters(), args.lr)
-    sch = oracle.ref_steplr(opt, int(args.steplr))
-    g = torch.Generator().manual_seed(4321)
-    xs = torch.rand(4, 1, 1, args.img, args.img, generator=g)
-    ts = (torch.rand(4, args.img, args.img, generator=g) > 0.5).float()
-    hebb = net.initialZeroHebb()
-    oracle.ref_train_step(net, opt, sch, xs[0], ts[0], hebb)          # warm-up sample
-    n, t0 = 0, time.perf_counter()
-    while True:
-        _, _, hebb = oracle.ref_train_step(net, opt, sch, xs[n % 4], ts[n % 4], hebb)
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= args.cpu_seconds and n >= 2) or n >= 200:
-            break
-    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
+
+    def run(bs, max_steps):
+        torch.manual_seed(0)
+        net = build_model(args, None, ref=True)
+        net.train()
+        opt = oracle.ref_adam(net.parameters(), args.lr)
+        sch = oracle.ref_steplr(opt, int(args.steplr))
+        g = torch.Generator().manual_seed(4321)
+        xs = torch.rand(2, bs, 1, args.img, args.img, generator=g)
+        ts = (torch.rand(2, bs, args.img, args.img, generator=g) > 0.5).float()
+        hebb = net.initialZeroHebb(bs) if bs > 1 else net.initialZeroHebb()
+        x0 = xs[0] if bs > 1 else xs[0, 0:1]
+        oracle.ref_train_step(net, opt, sch, x0, ts[0] if bs > 1 else ts[0, 0], hebb)     # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            k = n % 2
+            x, t = (xs[k], ts[k]) if bs > 1 else (xs[k, 0:1], ts[k, 0])
+            _, _, hebb = oracle.ref_train_step(net, opt, sch, x, t, hebb)
+            n += 1
+            el = time.perf_counter() - t0
+            if (el >= args.cpu_seconds and n >= 2) or n >= max_steps:
+                break
+        return n, el, type(net).__name__
+
+    n1, el1, name = run(1, 200)
+    nb, elb, _ = run(batch, 50)
+    return {"value": n1 / el1, "unit": "images/s", "cores": threads, "kind": "port",
             "sample": "oracle/ref_cpu.py %s %dx%d, reference mode (bs=1, fwd+BCE+bwd+Adam per sample, "
-                      "train.py:91-112): %d samples in %.1f s on %d threads"
-                      % (type(net).__name__, args.img, args.img, n, el, threads)}
+                      "train.py:91-112): %d samples in %.1f s on %d threads" % (name, args.img, args.img, n1, el1, threads),
+            "batched": {"value": nb * batch / elb, "unit": "images/s", "cores": threads, "kind": "port",
+                        "sample": "oracle/ref_cpu.py %s %dx%d, batched mode (bs=%d with per-slot traces "
+                                  "[%d,%d,%d] carried step to step, one Adam step per batch): %d steps = %d "
+                                  "images in %.1f s on %d threads"
+                                  % (name, args.img, args.img, batch, batch, args.img, args.img, nb, nb * batch,
+                                     elb, threads)}}
 
 
 def _launch_time_us(fn, reps):
@@ -305,6 +327,27 @@ def main():
         elapsed = max(per_rank)
     final_loss = loss.item() if loss is not None else float("nan")
 
+    # ---------------- all-reduce accounting (untimed pass): buckets issued, issued during the
+    # backward (overlapped), bucket sizes, and the exposed all-reduce time per step - the compute
+    # stream's wait between the last backward kernel and Adam (HIP events, punet/engine.py)
+    allreduce = {"active": False, "world": world,
+                 "note": "single rank: no gradient exchange (the reducer is off at world 1)"}
+    if trainer.reducer is not None:
+        trainer.measure_allreduce = True
+        trainer.allreduce_log = []
+        for i in range(max(2, min(5, args.steps))):
+            loss, hebb = trainer.step(xs[i % NB], ts[i % NB], hebb)
+        torch.cuda.synchronize()
+        trainer.measure_allreduce = False
+        allreduce = {"active": True, "world": world, "backend": dist.get_backend(),
+                     "op": "all_reduce AVG, async, issued from the backward as each bucket completes"}
+        allreduce.update(trainer.allreduce_info())
+        allreduce.update(trainer.allreduce_stats())
+        if world > 1:      # the slowest rank's exposure
+            t = torch.tensor([allreduce["exposed_ms_per_step"]], device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            allreduce["exposed_ms_per_step_max_rank"] = round(t.item(), 4)
+
     # ---------------- instrumented pass: per-launch HIP events on the launching stream
     kern = None
     roof = None
@@ -386,7 +429,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)
+        cpu = cpu_baseline(args, B)
 
     if rank == 0:
         value = world * B * args.steps / elapsed
@@ -416,6 +459,7 @@ def main():
             "final_loss": final_loss,
             "roofline": roof,
             "oja_update": oja,
+            "allreduce": allreduce,
             "cpu_baseline": cpu,
             "kernels": kern,
         }

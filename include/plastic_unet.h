@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define PU_ABI_VERSION 2
+#define PU_ABI_VERSION 3
 
 typedef enum {
     PU_OK = 0,

@@ -439,11 +439,22 @@ __global__ __launch_bounds__(HP_NT) void head_pipe_fwd_kernel(const T* __restric
     constexpr int RPP = 2 * PPI / N;          // stream rows per phase (4 with 8 streamer waves)
     constexpr int RPT = RPP / 2;              // rows per worker thread and phase
     static_assert(PPI % N == 0 && RPT <= 3, "a pass is whole rows");
+    static_assert(N / R == 8, "the XCD block order below assumes 8 row blocks per slot");
     __shared__ __attribute__((aligned(16))) float xs[(R + 1) * N];   // stream order: row 0, then own rows
     __shared__ __attribute__((aligned(16))) float ws[N * N];
     __shared__ float y0s[N];
-    const int b = blockIdx.y;
-    const int i0 = blockIdx.x * R;
+    // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs by linear id, so the
+    // plain (row block, slot) grid put row block x of EVERY slot on XCD x and each XCD's L2 fetched
+    // every slot's H_b (W_eff) and row-0 features - 8x per slot.  Unit u = xcd * B + (lin / 8)
+    // gives each XCD a contiguous run of units: the 8 row blocks of a slot share one XCD (B % 8 ==
+    // 0; otherwise at most one slot straddles two).  A bijection on [0, 8B): speed only, the
+    // per-block arithmetic does not depend on the placement.
+    const int nslot = gridDim.y;
+    const int lin = blockIdx.x + (N / R) * blockIdx.y;
+    const int unit = (lin & 7) * nslot + (lin >> 3);
+    const int b = unit / (N / R);
+    const int rb = unit % (N / R);
+    const int i0 = rb * R;
     const int tid = threadIdx.x;
     const bool streamer = tid < HP_SW;        // wave-uniform
     const long long nn = (long long)N * N;
@@ -454,7 +465,7 @@ __global__ __launch_bounds__(HP_NT) void head_pipe_fwd_kernel(const T* __restric
         const float bias = bo ? bo[0] : 0.f;
         const int lane = tid % L;
         // column rotation per block: the 256 blocks' streams start at staggered addresses
-        const int rot = PU_HP_ROT ? (int)((blockIdx.x * 8 + blockIdx.y) * 37u) & (N - 1) : 0;
+        const int rot = PU_HP_ROT ? (int)((rb * 8 + b) * 37u) & (N - 1) : 0;
         f32x4 buf[2][HP_U];
         // pixels of pass k (stream order q -> image row: q / N == 0 ? 0 : i0 + q / N - 1)
         auto load = [&](int k, f32x4 (&v)[HP_U]) {
@@ -849,7 +860,10 @@ extern "C" int pu_plastic_head_fwd(const pu_plastic_head_args* a, void* stream) 
         const char* e = getenv("PU_HEAD_PIPE");
         return !(e && e[0] == '0');
     }();
-    if (pipe_on && N == HP_N && L == 16 && a->hebb_out) {
+    // C >= 64: every streamer lane's first float4 (channels lane*4 .. lane*4+3 of the 16 lanes)
+    // and its outconv weights lie inside the pixel; C = 12, 24, 48, 60 also give L = 16 but would
+    // read the next pixel's channels (and past the end of wo / feat) - they take the serial kernel
+    if (pipe_on && N == HP_N && L == 16 && C >= 64 && a->hebb_out) {
         const dim3 pg(N / 16, a->batch);
         if (a->feat_bf16)
             hipLaunchKernelGGL((head_pipe_fwd_kernel<__bf16>), pg, dim3(HP_NT), 0, as_stream(stream), (const __bf16*)a->feat,

@@ -1617,11 +1617,14 @@ __global__ void wgrad_finish_kernel(const T* __restrict__ part, int G, int Nr, i
 }
 
 // wgrad_finish_kernel on quads of 4 consecutive entries of one slab row (Kc % 4 == 0): the same
-// 4 fp64 chains per entry in the same order (bit-identical), 8 partial quads in flight per thread
-// instead of 4 scalars.  The ConvT bias (mode 2: entries t*C + c of row N over every tap t and
-// partial g) runs as 4 chains over the flattened (t, g) sequence with 8 loads in flight - the
-// scalar form's one dependent chain of taps x G loads was a latency tail (17.7 us for a 64-channel
-// ConvT in C2).
+// 4 fp64 chains per entry in the same order - bit-identical to wgrad_finish_kernel for the WEIGHT
+// entries (and the bias of modes 0/1), 8 partial quads in flight per thread instead of 4 scalars.
+// The ConvT bias (mode 2: entries t*C + c of row N over every tap t and partial g) is NOT summed in
+// the scalar kernel's order: it runs as 4 interleaved fp64 chains over the flattened (t, g)
+// sequence with 8 loads in flight (the scalar form's one dependent chain of taps x G loads was a
+// latency tail, 17.7 us for a 64-channel ConvT in C2), so it can differ from the scalar kernel's
+// result in the last fp32 ulp.  It is deterministic run to run (fixed order; pinned by
+// tests/test_kernels_gpu.py::test_convT_bias_grad_run_to_run_bitwise).
 template <typename T>
 __global__ __launch_bounds__(256) void wgrad_finish4_kernel(const T* __restrict__ part, int G, int Nr, int Kc, int N,
                                                             int K, int C, int kh, int kw, int bias_mode,

@@ -23,7 +23,7 @@ PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD, PU
 PU_RULE_HEBB, PU_RULE_OJA = 0, 1
 
 
-ABI_VERSION = 2    # include/plastic_unet.h PU_ABI_VERSION
+ABI_VERSION = 3    # include/plastic_unet.h PU_ABI_VERSION
 
 
 class ConvArgs(ctypes.Structure):

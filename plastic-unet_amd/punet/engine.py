@@ -41,6 +41,51 @@ class Trainer:
             if self.distributed and overlap:
                 self.reducer = dp.BucketReducer(self.gradbuf, bucket_mb=bucket_mb, force=force_reduce)
         self.overlapped_buckets = 0
+        # all-reduce accounting (bench.py's `allreduce` block): set measure_allreduce = True and
+        # every step appends (buckets issued, issued during backward, exposed ms) to allreduce_log.
+        # Exposed time = the compute stream's wait for the collectives: a HIP event after the last
+        # backward kernel is enqueued and one after finish() has ordered the stream behind every
+        # bucket (on a CPU / gloo group: the host wall time of finish()).
+        self.measure_allreduce = False
+        self.allreduce_log = []
+
+    def allreduce_info(self):
+        """Static bucket layout of the overlapped reducer (None when it is not active)."""
+        if self.reducer is None:
+            return None
+        return {"buckets": len(self.reducer.buckets),
+                "bucket_mb": [round((e - s) * 4 / 1e6, 3) for s, e, _ in self.reducer.buckets],
+                "grad_mb": round(self.gradbuf.flat.numel() * 4 / 1e6, 3),
+                "nominal_bucket_mb": self.bucket_mb}
+
+    def allreduce_stats(self):
+        """Per-step averages over allreduce_log (call after the steps have been synchronised)."""
+        if not self.allreduce_log:
+            return None
+        n = len(self.allreduce_log)
+        exposed = []
+        for issued, early, ev in self.allreduce_log:
+            exposed.append(ev[0].elapsed_time(ev[1]) if isinstance(ev, tuple) else ev)
+        return {"steps": n, "buckets_issued": sum(r[0] for r in self.allreduce_log) / n,
+                "buckets_overlapped": sum(r[1] for r in self.allreduce_log) / n,
+                "exposed_ms_per_step": round(sum(exposed) / n, 4)}
+
+    def _finish_reduce(self):
+        if not self.measure_allreduce:
+            return self.reducer.finish()
+        import time
+        issued = len(self.reducer.buckets)
+        if self.gradbuf.flat.is_cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            early = self.reducer.finish()
+            e1.record()
+            self.allreduce_log.append((issued, early, (e0, e1)))
+        else:
+            t0 = time.perf_counter()
+            early = self.reducer.finish()
+            self.allreduce_log.append((issued, early, (time.perf_counter() - t0) * 1e3))
+        return early
 
     def step(self, x, t, hebb):
         """One optimisation step on the local batch.  Returns (loss tensor, new hebb), both
@@ -53,7 +98,7 @@ class Trainer:
             self.reducer.begin()          # buckets all-reduce (async) as the backward completes them
         loss.backward()
         if self.reducer is not None:
-            self.overlapped_buckets = self.reducer.finish()
+            self.overlapped_buckets = self._finish_reduce()
             if not self.gradbuf.owns_grads():       # grads did not land in the buffer: reduce them
                 dp.allreduce_grads(self.params, None)
         elif self.distributed:

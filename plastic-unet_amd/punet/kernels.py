@@ -370,6 +370,10 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
             n, c = (d0, d1) if mode == 0 else (d1, d0)
             out._wino = torch.empty(lib().pu_wino_bytes(n, c) // 2, dtype=BF16, device=w.device)
             pack_wino([(w, out._wino, mode == 1)])
+        elif hasattr(out, "_wino"):
+            # a U packed from the old weights must not outlive them: repacked in place with
+            # Winograd off, then Winograd back on, igemm would otherwise run on the stale U
+            del out._wino
     out._pack_spec = (mode, k_pad, cgroup)    # pack_weights() refreshes it in place
     return out
 

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     assert set(names) == bound, set(names) ^ bound
     for n in names:
         assert getattr(lib, n) is not None
-    assert lib.pu_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.pu_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_invalid_arguments_return_errors_without_gpu():

@@ -115,6 +115,7 @@ def _worker_nccl(rank, world, port, out_dir):
     xs, ts = _data()
     hebb = net.initialZeroHebb(B)
     out = {"loss": [], "grads": [], "overlapped": [], "owns": []}
+    tr.measure_allreduce = True       # bench.py's `allreduce` block (events only, no effect on results)
     for s in range(STEPS):
         loss, hebb = tr.step(xs[s].to(dev), ts[s].to(dev), hebb)
         out["owns"].append(tr.gradbuf.owns_grads())
@@ -123,6 +124,8 @@ def _worker_nccl(rank, world, port, out_dir):
                              if p.grad is not None})
         out["overlapped"].append(tr.overlapped_buckets)
     out["params"] = {n: p.detach().cpu().clone() for n, p in net.named_parameters()}
+    torch.cuda.synchronize()
+    out["ar_info"], out["ar_stats"] = tr.allreduce_info(), tr.allreduce_stats()
     torch.save(out, os.path.join(out_dir, "nccl.pt"))
     dist.destroy_process_group()
 
@@ -149,6 +152,13 @@ def test_rccl_async_bucket_path_world1(tmp_path, gpu_device):
     r = torch.load(os.path.join(tmp_path, "nccl.pt"), weights_only=True)
     assert all(r["owns"]), r["owns"]
     assert all(o >= 2 for o in r["overlapped"]), r["overlapped"]
+    # the bench's `allreduce` block: layout, per-step counts and a non-negative exposed time
+    info, st = r["ar_info"], r["ar_stats"]
+    assert info["buckets"] >= 2 and len(info["bucket_mb"]) == info["buckets"]
+    assert abs(sum(info["bucket_mb"]) - info["grad_mb"]) < 1e-3 * (info["buckets"] + 1)
+    assert st["steps"] == STEPS and st["buckets_issued"] == info["buckets"]
+    assert 2 <= st["buckets_overlapped"] <= st["buckets_issued"]
+    assert 0.0 <= st["exposed_ms_per_step"] < 1e3
     assert r["loss"] == ref_loss
     for s in range(STEPS):
         for n, g in ref_grads[s].items():

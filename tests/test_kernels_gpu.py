@@ -201,6 +201,24 @@ def test_convT2x2(B, h, cin, cout):
     assert_close(db, b.grad)
 
 
+@pytest.mark.parametrize("B,h,cin,cout", [(3, 8, 64, 64), (2, 16, 128, 128), (4, 32, 64, 64)])
+def test_convT_bias_grad_run_to_run_bitwise(B, h, cin, cout):
+    """The ConvT bias gradient (wgrad_finish4_kernel bias_mode 2: 4 interleaved fp64 chains over the
+    flattened (tap, split) sequence) is deterministic: two runs agree bit for bit, weights included,
+    and both match the torch gradient."""
+    g = torch.Generator().manual_seed(h * 11 + cin)
+    x = rnd(B, cin, h, h, g=g).relu()
+    gu = rnd(B, cout, 2 * h, 2 * h, g=g)
+    xk, guk = nhwc(x).to(DEV), nhwc(gu).to(DEV)
+    dw, db = T.convT2x2_wgrad(xk, guk)
+    dw2, db2 = T.convT2x2_wgrad(xk, guk)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    assert_close(db, gu.sum((0, 2, 3)))
+    wr = torch.zeros(cin, cout, 2, 2, requires_grad=True)
+    F.conv_transpose2d(x, wr, stride=2).backward(gu)
+    assert_close(dw, wr.grad)
+
+
 @pytest.mark.parametrize("B,H,W,C", [(2, 8, 8, 16), (1, 7, 9, 3), (2, 16, 16, 64)])
 def test_maxpool(B, H, W, C):
     g = torch.Generator().manual_seed(H * W + C)
@@ -415,7 +433,13 @@ def test_fused_head_trace_equals_two_launch_path(B, N, rule):
                                       # fallback at N = 272
                                       (2, 256, 16, torch.bfloat16), (1, 272, 8, torch.float32),
                                       # the pipelined single-chunk path (C == 4 L) at every L
-                                      (4, 64, 4, torch.float32), (2, 112, 32, torch.bfloat16)])
+                                      (4, 64, 4, torch.float32), (2, 112, 32, torch.bfloat16),
+                                      # N = 128 with C = 48: L = 16 lanes but C < 64 - the serial
+                                      # kernel (the pipelined one would read the next pixel)
+                                      (2, 128, 48, torch.float32), (2, 128, 48, torch.bfloat16),
+                                      # the pipelined kernel's XCD block order: B % 8 == 0 (each
+                                      # slot on one XCD) and B = 9 (one slot straddles two)
+                                      (32, 128, 64, torch.float32), (9, 128, 96, torch.bfloat16)])
 def test_fused_head_equals_outconv_then_head(rule, B, N, C, dt):
     """pu_plastic_head_fwd (outconv + Weff GEMM on v_mfma_f32_16x16x4_f32 + sigmoid + trace update,
     one launch) is bit-identical to the two-kernel path outconv_fwd -> plastic_fwd: the outconv sum

@@ -47,7 +47,8 @@ H = (0.05 * torch.randn(3, 64, 64, generator=g)).to(dev)
 y, hn = net(x, H)
 bce_loss(y, t).backward()
 torch.cuda.synchronize()
-out = {"lib": os.path.basename(_lib.LIB_PATH), "y": y.double().sum().item(), "h": hn.double().sum().item()}
+out = {"lib": os.path.basename(_lib.LIB_PATH), "bid": _lib.build_id(), "y": y.double().sum().item(),
+       "h": hn.double().sum().item()}
 out.update({k: p.grad.double().abs().sum().item() for k, p in net.named_parameters() if p.grad is not None})
 print("RESULT " + json.dumps(out))
 """
@@ -70,7 +71,15 @@ def test_pu_debug_library_matches_release():
     rel = os.path.join(PKG, "lib", "libplastic_unet.so")
     if not os.path.exists(dbg):
         pytest.fail("debug library missing: build it with build_native.py --variant debug (build() does)")
+    import build_native
     a, b = _run_step(rel), _run_step(dbg)
     assert a["lib"] == "libplastic_unet.so" and b["lib"] == "libplastic_unet_debug.so"
-    a.pop("lib"), b.pop("lib")
+    # both libraries must be builds of THIS tree's sources: a stale variant (built before the last
+    # source change) would compare different kernels and fail for the wrong reason (round 4 r04b)
+    want_rel, want_dbg = build_native.source_hash(), build_native.source_hash(("PU_DEBUG=1",))
+    assert a["bid"] == want_rel, "release library is stale (build id %s, sources %s): rebuild" % (a["bid"], want_rel)
+    assert b["bid"] == want_dbg, ("debug library is stale (build id %s, sources %s): "
+                                  "build_native.py --variant debug" % (b["bid"], want_dbg))
+    for r in (a, b):
+        r.pop("lib"), r.pop("bid")
     assert a == b
