@@ -39,10 +39,12 @@
 #define PU_NO_ILV 0   // 1: leave MFMA / VALU placement to the scheduler (A/B builds)
 #endif
 // wino_x6_kernel ablations (timing only, wrong results): 1 no MFMAs, 2 no V formation (VALU + LDS
-// stores), 3 no window loads, 4 no per-sub-stage barrier (the waits stay), 5 no U DMA
+// stores), 3 no window loads, 4 no per-sub-stage barrier (the waits stay), 5 no U DMA, 6 no output
+// stores, 7 no bias loads
 #ifndef PU_WF_ABL
 #define PU_WF_ABL 0
 #endif
+
 
 namespace pu {
 
@@ -87,6 +89,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
 // (past the last item the buffer range is empty and zeros land), so the wait counts are
 // compile-time exact: issued after U(s) are the window rows of s-3, s-2, s-1 (4 / 4 / 8 / 0 row
 // loads in sub-stages i = 0 / 1 / 2 / 3) and U(s+1), U(s+2) (3 pieces each).
+#ifndef PU_WPP_STAMP
+#define PU_WPP_STAMP 0     // diagnostic build: block 0's per-wave s_memtime before / after every barrier
+#endif
+#if PU_WPP_STAMP
+constexpr int PU_WPP_NSTAMP = 512;
+__device__ unsigned long long pu_wpp_stamp_buf[8 * PU_WPP_NSTAMP];
+// lane 0 of block 0's waves: shader-clock stamp k of wave w (diagnostic builds only; the stamp
+// stores are vector-memory ops and shift the kernel's counted vmcnt waits - timing only)
+__device__ __forceinline__ void wpp_stamp_at(int wave, int& n) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && n < PU_WPP_NSTAMP) pu_wpp_stamp_buf[wave * PU_WPP_NSTAMP + n] = t;
+    ++n;
+}
+#define WPP_STAMP(w, n) wpp_stamp_at(w, n)
+#else
+#define WPP_STAMP(w, n) ((void)0)
+#endif
 template <bool PERSIST>
 __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 #pragma clang fp contract(off)
@@ -104,6 +123,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave & 1, wn = (wave >> 1) & 1, wx = wave >> 2;
+    int nst = 0;
     const int per_split = w.gm * p.gn;
     const int total = per_split * p.ksplit;
 
@@ -283,7 +303,9 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         else if constexpr (i == 1) asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
         else if constexpr (i == 2) asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(22) lgkmcnt(0)" ::: "memory");
+        WPP_STAMP(wave, nst);
         if (PU_WF_ABL != 4) __builtin_amdgcn_s_barrier();
+        WPP_STAMP(wave, nst);
         asm volatile("" ::: "memory");
         if constexpr (i == 0) load_u(cur, kc, 3, fu);
         else load_u(T, tkc, i - 1, fu);
@@ -346,7 +368,9 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
         }
         // every wave is past the last sub-stage's reads of V slot 1 and its V stores are done
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        WPP_STAMP(wave, nst);
         __builtin_amdgcn_s_barrier();
+        WPP_STAMP(wave, nst);
         asm volatile("" ::: "memory");
 
         // ---- output transform Y = A^T M A.  Wave wx holds positions j = 2wx, 2wx+1 of every
@@ -378,7 +402,9 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
                 }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            WPP_STAMP(wave, nst);
             __builtin_amdgcn_s_barrier();
+            WPP_STAMP(wave, nst);
             asm volatile("" ::: "memory");
 #pragma unroll
             for (int r4 = 0; r4 < 4; ++r4) {
@@ -393,7 +419,9 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
                 }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            WPP_STAMP(wave, nst);
             __builtin_amdgcn_s_barrier();
+            WPP_STAMP(wave, nst);
             asm volatile("" ::: "memory");
         }
         const int e_m = cur.m_blk + 32 * wm + (lane & 31), e_n = cur.n_blk + 32 * wn + 4 * (lane >> 5);
@@ -419,7 +447,7 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
                     const long long o0 = first ? r0 + n : r1 + (n - p.n0);
                     f32x4 y[2] = {{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]},
                                   {y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]}};
-                    const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+                    const f32x4 bv = p.bias && PU_WF_ABL != 7 ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int o = 0; o < 2; ++o) {
                         const long long off = o0 + o * ld;
@@ -437,7 +465,11 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
                         }
                         if (p.cscale) v *= *reinterpret_cast<const f32x4*>(p.cscale + (long long)b * p.cs_ld + n);
                         if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
-                        *reinterpret_cast<f32x4*>(dst + off) = v;
+                        if (PU_WF_ABL == 6) {      // no output stores (timing only): keep v alive
+                            if (v[0] == 1.2345e-30f) *reinterpret_cast<f32x4*>(dst + off) = v;
+                        } else {
+                            *reinterpret_cast<f32x4*>(dst + off) = v;
+                        }
                     }
                 }
             } else {
@@ -638,6 +670,15 @@ size_t wino_workspace_bytes(const pu_conv_args* a) {
 }  // namespace pu
 
 using namespace pu;
+
+#if PU_WPP_STAMP
+// diagnostic build only: copy block 0's barrier stamps ([8 waves][PU_WPP_NSTAMP] shader cycles)
+extern "C" int pu_wpp_stamps(unsigned long long* dst, int n) {
+    if (n > 8 * PU_WPP_NSTAMP) n = 8 * PU_WPP_NSTAMP;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(pu_wpp_stamp_buf), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? n : -1;
+}
+#endif
 
 extern "C" size_t pu_wino_bytes(int n, int c) {
     return (n > 0 && c > 0 && c % 16 == 0) ? (size_t)n * c * 96 : 0;
