@@ -421,7 +421,10 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
 #ifndef PU_HP_ROT
 #define PU_HP_ROT 1
 #endif
-constexpr int HP_SW = PU_HP_SW * 64, HP_NT = HP_SW + 256, HP_U = 8, HP_N = 128;
+#ifndef PU_HP_U
+#define PU_HP_U 8          // pixels in flight per streamer lane group and pass
+#endif
+constexpr int HP_SW = PU_HP_SW * 64, HP_NT = HP_SW + 256, HP_U = PU_HP_U, HP_N = 128;
 template <typename T>
 __global__ __launch_bounds__(HP_NT) void head_pipe_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ wo,
                                                               const float* __restrict__ bo, int C,
