@@ -28,7 +28,7 @@ def smi():
         out = {}
         for k, v in card.items():
             kl = k.lower()
-            if "sclk" in kl and "clock" in kl:
+            if "sclk" in kl and "speed" in kl:
                 out["sclk"] = v
             elif "power" in kl:
                 out["power"] = v
