@@ -18,10 +18,28 @@ outconv-bwd multiply by (activation > 0)), writes skip gradients once and lets t
 backward accumulate into them, and gets bias gradients from the weight-gradient GEMM (a ones
 column / ones row), so no separate elementwise or reduction passes run.
 """
+import os
+
 import torch
 
 from . import kernels as K
 from ._lib import PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD
+
+
+# Weight-gradient side stream: the backward enqueues every weight gradient (and its split
+# reduction) on a second stream, ordered after the kernel that produced its dZ, so they overlap the
+# data-gradient chain.  PU_WSTREAM=1 always, 0 never, unset: bf16 trunks only - measured
+# (profiles/r05_experiments/side_stream_ab.txt): C3 (bf16) 8822 -> 8952 img/s, C2 (fp32) 4370 ->
+# 4317: the fp32 Winograd kernels hold a whole CU per block (LDS + 2 x 256 VGPRs per SIMD), so
+# concurrent launches only queue behind each other and slow both.
+_SIDE = {"1": True, "0": False}.get(os.environ.get("PU_WSTREAM", ""), "bf16")
+
+
+def set_side_stream(on):
+    """Switch the weight-gradient side stream for backward passes started after this call:
+    True / False, or "bf16" (the default: bf16 trunks only)."""
+    global _SIDE
+    _SIDE = on if on == "bf16" else bool(on)
 
 
 class _Packs:
@@ -253,6 +271,8 @@ class UNetpTrunk:
         # True: forward returns the last activation (the outconv runs inside the fused head,
         # punet.head.FusedHeadFunction) and backward receives dL/d(its pre-ReLU) from the head
         self.fused_head = False
+        self._ws = None          # weight-gradient side stream (PU_WSTREAM), created on first use
+        self._side = None        # the side stream while a backward runs with it, else None
 
     def backward_order(self):
         """Parameters in the order backward() completes their gradients (outc first, stem last;
@@ -272,10 +292,41 @@ class UNetpTrunk:
         return order
 
     def _ready(self, i, n=2):
-        """params[i:i+n]'s gradient kernels are enqueued: let an armed BucketReducer know."""
+        """params[i:i+n]'s gradient kernels are enqueued: let an armed BucketReducer know.  With
+        the side stream the bucket is issued from it (RCCL then orders after the stream's weight
+        gradients), after the stream has caught up with the compute stream (BatchNorm grads)."""
         gb = self.gradbuf
-        if gb is not None and gb.reducer is not None:
+        if gb is None or gb.reducer is None:
+            return
+        ws = self._side
+        if ws is None:
             gb.ready(*self.params[i:i + n])
+            return
+        ws.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(ws):
+            gb.ready(*self.params[i:i + n])
+
+    def _wgrad(self, fn, i, out, *reads):
+        """Run weight-gradient launcher fn(out) for params[i:i+2] - on the side stream when one is
+        active: the stream waits for the compute stream (dZ is its last kernel), the outputs are
+        allocated on the compute stream (autograd and the optimizer use them there) and every
+        tensor the side stream reads is recorded against it, so the caching allocator does not
+        hand its memory out again before the side stream is done with it."""
+        ws = self._side
+        if ws is None:
+            r = fn(out)
+        else:
+            if out is None:
+                out = (torch.empty_like(self.params[i], memory_format=torch.contiguous_format),
+                       torch.empty_like(self.params[i + 1]))
+            ws.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(ws):
+                r = fn(out)
+            for t in reads:
+                if t is not None:
+                    t.record_stream(ws)
+        self._ready(i)
+        return r
 
     def grad_sinks(self):
         """Views of the flat gradient buffer to write into, or None.  Only used when every
@@ -370,6 +421,18 @@ class UNetpTrunk:
         return dz
 
     def backward(self, s, dlogits, params):
+        if dlogits.is_cuda and (_SIDE is True or (_SIDE == "bf16" and self.dtype == torch.bfloat16)):
+            if self._ws is None or self._ws.device != dlogits.device:
+                self._ws = torch.cuda.Stream(device=dlogits.device)
+            self._side = self._ws
+        try:
+            return self._backward(s, dlogits, params)
+        finally:
+            if self._side is not None:
+                torch.cuda.current_stream().wait_stream(self._side)   # grads complete before use
+                self._side = None
+
+    def _backward(self, s, dlogits, params):
         D = self.depth
         pk = self.packs
         P = list(params)
@@ -402,18 +465,17 @@ class UNetpTrunk:
                 self.debug["up%d.c1" % j] = g
             # conv1 of up_j: y_j = relu([bn](conv(t)));  g = dL/d(pre-ReLU)
             g = self._bn_back("up%d.c1" % j, g, s, P, grads, out)
-            grads[c1], grads[c1 + 1] = conv3x3_wgrad(g, t, out=out(c1))
-            self._ready(c1)
+            grads[c1], grads[c1 + 1] = self._wgrad(lambda o: conv3x3_wgrad(g, t, out=o), c1, out(c1), g, t)
             dt, _ = conv3x3_dgrad(g, P[c1], pk, mask0=t)
             dt = self._bn_back("up%d.c0" % j, dt, s, P, grads, out)
             # conv0 over [skip | u]  (up_first: [u | skip])
             if self.up_first:
-                grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, u, skip, out=out(c0))
-                self._ready(c0)
+                grads[c0], grads[c0 + 1] = self._wgrad(lambda o: conv3x3_wgrad(dt, u, skip, out=o), c0, out(c0),
+                                                       dt, u, skip)
                 du, dskip = conv3x3_dgrad(dt, P[c0], pk, split=u.shape[3], mask1=skip)
             else:
-                grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, skip, u, out=out(c0))
-                self._ready(c0)
+                grads[c0], grads[c0 + 1] = self._wgrad(lambda o: conv3x3_wgrad(dt, skip, u, out=o), c0, out(c0),
+                                                       dt, skip, u)
                 dskip, du = conv3x3_dgrad(dt, P[c0], pk, split=skip.shape[3], mask0=skip)
             if self.debug is not None:
                 self.debug["up%d.c0" % j] = dt
@@ -423,8 +485,8 @@ class UNetpTrunk:
                 g = K.upsample_bilinear2x_bwd(du, mask=y_prev)
             else:
                 ui = sl["up%d.up" % j]
-                grads[ui], grads[ui + 1] = convT2x2_wgrad(y_prev, du, out=out(ui))
-                self._ready(ui)
+                grads[ui], grads[ui + 1] = self._wgrad(lambda o: convT2x2_wgrad(y_prev, du, out=o), ui, out(ui),
+                                                       y_prev, du)
                 g = convT2x2_dgrad(du, P[ui], pk, mask=y_prev)
 
         for i in range(D - 1, 0, -1):
@@ -434,12 +496,10 @@ class UNetpTrunk:
             if self.debug is not None:
                 self.debug["down%d.c1" % i] = g
             g = self._bn_back("down%d.c1" % i, g, s, P, grads, out)
-            grads[c1], grads[c1 + 1] = conv3x3_wgrad(g, t, out=out(c1))
-            self._ready(c1)
+            grads[c1], grads[c1 + 1] = self._wgrad(lambda o: conv3x3_wgrad(g, t, out=o), c1, out(c1), g, t)
             dt, _ = conv3x3_dgrad(g, P[c1], pk, mask0=t)
             dt = self._bn_back("down%d.c0" % i, dt, s, P, grads, out)
-            grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, p, out=out(c0))
-            self._ready(c0)
+            grads[c0], grads[c0 + 1] = self._wgrad(lambda o: conv3x3_wgrad(dt, p, out=o), c0, out(c0), dt, p)
             if self.debug is not None:
                 self.debug["down%d.c0" % i] = dt
             dp, _ = conv3x3_dgrad(dt, P[c0], pk)
@@ -450,15 +510,13 @@ class UNetpTrunk:
         if self.debug is not None:
             self.debug["inc.c1"] = g
         g = self._bn_back("inc.c1", g, s, P, grads, out)
-        grads[c1], grads[c1 + 1] = conv3x3_wgrad(g, t, out=out(c1))
-        self._ready(c1)
+        grads[c1], grads[c1 + 1] = self._wgrad(lambda o: conv3x3_wgrad(g, t, out=o), c1, out(c1), g, t)
         dt, _ = conv3x3_dgrad(g, P[c1], pk, mask0=t)
         x0 = s["stem"] if self.coord is not None else s["x"]
         if dt.dtype != x0.dtype:       # bf16 trunk: the fp32 stem's weight gradient
             dt = K.to_f32(dt)
         dt = self._bn_back("inc.c0", dt, s, P, grads, out)
-        grads[c0], grads[c0 + 1] = conv3x3_wgrad(dt, x0, out=out(c0))
-        self._ready(c0)
+        grads[c0], grads[c0 + 1] = self._wgrad(lambda o: conv3x3_wgrad(dt, x0, out=o), c0, out(c0), dt, x0)
         if self.debug is not None:
             self.debug["inc.c0"] = dt
         if self.coord is not None:     # stem 1x1 conv: dgrad of inc.c0 (masked by the stem ReLU) + wgrad
@@ -468,10 +526,12 @@ class UNetpTrunk:
             o = out(cs)
             dw = torch.empty(P[cs].shape, dtype=torch.float32, device=dt.device) if o is None else o[0]
             db = torch.empty(P[cs + 1].shape, dtype=torch.float32, device=dt.device) if o is None else o[1]
-            K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, rows=dstem, n=P[cs].shape[0],
-                    src0=s["x"], c0=ca, bias_mode=1, dweight=dw, dbias=db)
-            grads[cs], grads[cs + 1] = dw, db
-            self._ready(cs)
+
+            def stem_wgrad(o):
+                K.wgrad(batch=B, in_hw=(H, W), out_hw=(H, W), k=1, stride=1, pad=0, rows=dstem,
+                        n=P[cs].shape[0], src0=s["x"], c0=ca, bias_mode=1, dweight=o[0], dbias=o[1])
+                return o
+            grads[cs], grads[cs + 1] = self._wgrad(stem_wgrad, cs, (dw, db), dstem, s["x"])
         return grads
 
 

@@ -99,11 +99,13 @@ def test_overlapped_dp_matches_single_process(tmp_path, gpu_device):
     torch.testing.assert_close(torch.cat([r["hebb"] for r in res]), ref["hebb"], rtol=1e-4, atol=1e-6)
 
 
-def _worker_nccl(rank, world, port, out_dir):
+def _worker_nccl(rank, world, port, out_dir, side=False):
     import sys
     for p in (ROOT, PKG):
         if p not in sys.path:
             sys.path.insert(0, p)
+    from punet import trunk
+    trunk.set_side_stream(side)       # weight gradients (and bucket issue) on the trunk's side stream
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     from punet.engine import Trainer
@@ -130,12 +132,14 @@ def _worker_nccl(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_rccl_async_bucket_path_world1(tmp_path, gpu_device):
+@pytest.mark.parametrize("side", [False, True])
+def test_rccl_async_bucket_path_world1(tmp_path, gpu_device, side):
     """The production RCCL path of BucketReducer (ReduceOp.AVG, async_op all-reduces issued from
     the autograd thread on RCCL's stream, finish() ordering the compute stream by work.wait()) in
     a world of one rank: AVG over one rank is the identity, so two steps must reproduce the
     no-reducer run bit for bit - a missing stream dependency would let Adam read gradients the
-    collective is still writing."""
+    collective is still writing.  side=True: the weight gradients run on the trunk's side stream
+    (PU_WSTREAM) and the buckets are issued from it; the reference run keeps one stream."""
     from punet.engine import Trainer
     torch.manual_seed(0)
     net = _ctor(gpu_device)
@@ -148,7 +152,7 @@ def test_rccl_async_bucket_path_world1(tmp_path, gpu_device):
         ref_loss.append(loss.item())
         ref_grads.append({n: p.grad.detach().cpu().clone() for n, p in net.named_parameters() if p.grad is not None})
     ref_params = {n: p.detach().cpu().clone() for n, p in net.named_parameters()}
-    mp.spawn(_worker_nccl, args=(1, _free_port(), str(tmp_path)), nprocs=1, join=True)
+    mp.spawn(_worker_nccl, args=(1, _free_port(), str(tmp_path), side), nprocs=1, join=True)
     r = torch.load(os.path.join(tmp_path, "nccl.pt"), weights_only=True)
     assert all(r["owns"]), r["owns"]
     assert all(o >= 2 for o in r["overlapped"]), r["overlapped"]

@@ -347,3 +347,42 @@ def test_forward_after_optimizer_step_sees_new_weights():
     y2, h2 = fresh(x, h0)
     assert not torch.equal(y1, y0)
     assert torch.equal(y1, y2) and torch.equal(h1, h2)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c2_side_stream_weight_gradients_bitwise(precision):
+    """PU_WSTREAM: the trunk's weight gradients run on a second stream beside the data-gradient
+    chain (the default for bf16 trunks, C3).  Three Trainer steps at C2/C3 widths (bs 8) must match
+    the one-stream run bit for bit - losses, every gradient and the updated parameters (a missing
+    dependency or an allocator reuse race would show up as a difference)."""
+    from punet import trunk
+    from punet.engine import Trainer
+    res = []
+    for side in (False, True):
+        trunk.set_side_stream(side)
+        try:
+            _, net, x, t, H = _c2_pair(8, seed=3)
+            if precision == "bf16":
+                sd = net.state_dict()
+                net = UNetp(1, 1, DEV, rule="oja", nbf=128, depth=5, base_ch=64, precision="bf16")
+                net.load_state_dict(sd)
+            tr = Trainer(net, lr=1e-3, steplr=1e5)
+            hebb = H.to(DEV)
+            losses, grads = [], []
+            for s in range(3):
+                xs = torch.roll(x, shifts=s, dims=0).to(DEV)
+                loss, hebb = tr.step(xs, t.to(DEV), hebb)
+                losses.append(loss.item())
+                grads.append({k: p.grad.detach().clone() for k, p in net.named_parameters() if p.grad is not None})
+            torch.cuda.synchronize()
+            res.append((losses, grads, {k: p.detach().clone() for k, p in net.named_parameters()}, hebb.clone()))
+        finally:
+            trunk.set_side_stream("bf16")
+    assert res[0][0] == res[1][0]
+    for s in range(3):
+        assert res[0][1][s].keys() == res[1][1][s].keys()
+        for k in res[0][1][s]:
+            assert torch.equal(res[0][1][s][k], res[1][1][s][k]), (s, k)
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
+    assert torch.equal(res[0][3], res[1][3])
