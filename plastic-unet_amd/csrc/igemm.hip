@@ -15,6 +15,10 @@
 #include <type_traits>
 
 
+#ifndef PU_EPI_BATCH
+#define PU_EPI_BATCH 1   // 0: every output through epi_store4 (A/B builds)
+#endif
+
 namespace pu {
 
 
@@ -63,11 +67,109 @@ __device__ __forceinline__ f32x4 load_a4(const IgemmParams& p, int pb, int hb, i
 }
 
 
-template <int BM, int BN, int WM, int WN>
+// The epilogue's two common forms - bias (+ReLU), the forward, or masks (+ReLU), the data
+// gradient, into one or two NHWC destinations - with every operand load issued before the first
+// store.  gfx9's vmcnt counts stores as well as loads, and epi_store4 loads each output's operand
+// right before its store: the wait for that load then also waited out the round trip of every
+// store before it, one store latency per output.  Operands and stores go through buffer
+// descriptors with 32-bit offsets (a 32-column fragment lies in one destination: n0 % 32 == 0,
+// so the descriptor is wave-uniform per fragment); lanes past M / N load zeros and drop their
+// stores (out-of-range offsets), so no per-lane branch splits the batch.  The bias is per channel:
+// MASK == false reads it per fragment column group.  Same operations in the same order as
+// epi_store4 (bias, ReLU, mask).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t epi_rsrc(const void* base, bool on) {
+    const unsigned long long b = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(ub, 0, on ? 0x7fffffff : 0, 0x00020000);
+}
+
+template <bool MASK, int FM, int FN>
+__device__ __forceinline__ void epilogue_batched(const IgemmParams& p, f32x16 (&acc)[FM][FN], int m0, int nc0, int lr,
+                                                 int lh) {
+    const bool relu = p.flags & PU_EPI_RELU;
+    const int n1 = p.N - p.n0;
+    unsigned orow[FM][FN];             // byte offset of (row m, fragment column 0), LEAN_OOB past M
+    bool first[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) first[j] = nc0 + j * 32 < p.n0;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+        const int m = m0 + i * 32 + lr;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+            const int c = nc0 + j * 32 + 4 * lh - (first[j] ? 0 : p.n0);
+            orow[i][j] = m < p.M && nc0 + j * 32 < p.N ? (unsigned)(m * (first[j] ? p.n0 : n1) + c) * 4u : LEAN_OOB;
+        }
+    }
+    f32x4 ov[FM][FN][4];               // MASK: the mask of each output; else the bias of its channels
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        if constexpr (MASK) {
+            const float* mk = first[j] ? p.mask0 : p.mask1;
+            const __amdgpu_buffer_rsrc_t r = epi_rsrc(mk, mk != nullptr);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    ov[i][j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, orow[i][j], 32 * q, 0));
+        } else {
+            const __amdgpu_buffer_rsrc_t r = epi_rsrc(p.bias, true);
+            const unsigned nb = nc0 + j * 32 < p.N ? (unsigned)(nc0 + j * 32 + 4 * lh) * 4u : LEAN_OOB;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                ov[0][j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, nb, 32 * q, 0));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const __amdgpu_buffer_rsrc_t rd = epi_rsrc(first[j] ? p.dst0 : p.dst1, true);
+        const bool has_mk = (first[j] ? p.mask0 : p.mask1) != nullptr;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                if constexpr (!MASK) v += ov[0][j][q];
+                if (relu) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                }
+                if constexpr (MASK) {
+                    if (has_mk) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) if (!(ov[i][j][q][e] > 0.f)) v[e] = 0.f;
+                    }
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rd, orow[i][j], 32 * q, 0);
+            }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool BATCH = false>
 __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m_blk,
                                          int n_blk, int wm, int wn, int lr, int lh) {
     constexpr int FM = BM / WM / 32;
     constexpr int FN = BN / WN / 32;
+    if constexpr (BATCH && PU_EPI_BATCH) {
+        // 32-column fragments never straddle n0; every destination byte offset fits 31 bits
+        if (p.vec_epi && !(p.flags & (PU_EPI_SHUFFLE2 | PU_EPI_ACCUM)) && !p.resid && !p.cscale && p.n0 % 32 == 0 &&
+            p.N % 32 == 0 && (long long)p.M * p.N < (1LL << 29)) {
+            const int m0 = m_blk + wm * (BM / WM), nc0 = n_blk + wn * (BN / WN);
+            if ((p.mask0 || p.mask1) && !p.bias) {
+                epilogue_batched<true, FM, FN>(p, acc, m0, nc0, lr, lh);
+                return;
+            }
+            if (!p.mask0 && !p.mask1 && p.bias) {
+                epilogue_batched<false, FM, FN>(p, acc, m0, nc0, lr, lh);
+                return;
+            }
+        }
+    }
     // ---- epilogue.  acc[i][j] = D^T block: MFMA row = channel n = 8*(r>>2) + 4*(lane>>5) + (r&3),
     // column = pixel m = lane & 31.  Registers 4q..4q+3 are 4 consecutive channels of one pixel:
     // bias / ReLU / mask / accumulate / store run on float4 (16 B per lane).
@@ -663,7 +765,7 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_kernel(const IgemmParams p) 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (p.ksplit == 1) {
-        epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
+        epilogue<BM, BN, WM, WN, true>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
         return;
     }
     float* part = p.part + (long long)kz * p.M * p.N;
@@ -870,7 +972,7 @@ __global__ __launch_bounds__(NW * 64) void igemm_x6_lean_kernel(const IgemmParam
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (p.ksplit == 1) {
-        epilogue<BM, BN, WM, WN>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
+        epilogue<BM, BN, WM, WN, true>(p, acc, m_blk, n_blk, wm, wn, lr, lh);
         return;
     }
     float* part = p.part + (long long)kz * p.M * p.N;

@@ -75,6 +75,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
     return __builtin_amdgcn_make_buffer_rsrc(ub, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// epilogue operand load / store through a buffer descriptor (out-of-range offsets: zeros / dropped)
+__device__ __forceinline__ f32x4 epi_ld4(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void epi_st4(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
 // One block walks work items (tile block x channel block x K split): PERSIST - one block per CU,
 // each XCD a contiguous range of items, channel block slowest (the items an XCD runs at once share
 // one U slice in its L2); otherwise one item per block (XCD-aware order).
@@ -425,60 +433,91 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
             asm volatile("" ::: "memory");
         }
         const int e_m = cur.m_blk + 32 * wm + (lane & 31), e_n = cur.n_blk + 32 * wn + 4 * (lane >> 5);
-        if (e_m < w.tiles) {
-            const int t2 = fdiv(e_m, w.dTw);
-            const int tx = e_m - t2 * (p.Wo >> 1);
-            const int b = fdiv(t2, w.dTh);
-            const int ty = t2 - b * (p.Ho >> 1);
-            const long long pix0 = ((long long)b * p.Ho + 2 * ty + wx) * p.Wo + 2 * tx;
-            if (p.ksplit == 1) {
-                // igemm's float4 epilogue (epi_store4) for the lane's two pixels, with the row
-                // offsets of both destinations formed once
-                const int n1 = p.N - p.n0;
-                const long long r0 = pix0 * p.n0, r1 = pix0 * n1;
-                const bool relu = p.flags & PU_EPI_RELU, accum = p.flags & PU_EPI_ACCUM;
+        const bool e_ok = e_m < w.tiles;
+        const int em = e_ok ? e_m : 0;
+        const int t2 = fdiv(em, w.dTw);
+        const int tx = em - t2 * (p.Wo >> 1);
+        const int b = fdiv(t2, w.dTh);
+        const int ty = t2 - b * (p.Ho >> 1);
+        const long long pix0 = ((long long)b * p.Ho + 2 * ty + wx) * p.Wo + 2 * tx;
+        if (p.ksplit == 1) {
+            // igemm's float4 epilogue (bias, residual, ReLU, mask, channel scale, accumulate) for
+            // the lane's two pixels.  Every operand load is issued, unconditionally and back to
+            // back, before the first store: gfx9's vmcnt counts stores too, so a load issued after
+            // a store (and waited for) waits out that store's round trip - with the loads inside
+            // the per-flag branches each of the 8 stores was followed by a vmcnt(0).  Absent
+            // operands read through an empty buffer range (no memory traffic); lanes past the
+            // last tile load and store out of range.  A 64-channel item lies in one destination
+            // (wino_ok: n0 % 64 == 0), so the destination is item-uniform.
+            const bool first = cur.n_blk < p.n0;
+            const int ld = first ? p.n0 : p.N - p.n0;
+            float* dst = first ? p.dst0 : p.dst1;
+            const float* msk = first ? p.mask0 : p.mask1;
+            const bool relu = p.flags & PU_EPI_RELU, accum = p.flags & PU_EPI_ACCUM;
+            constexpr unsigned FULL = 0x7fffffffu;
+            const __amdgpu_buffer_rsrc_t r_dst = uniform_rsrc(dst, FULL);
+            const __amdgpu_buffer_rsrc_t r_acc = uniform_rsrc(dst, accum ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_res = uniform_rsrc(p.resid, p.resid ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_msk = uniform_rsrc(msk, msk ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_bias = uniform_rsrc(p.bias, p.bias && PU_WF_ABL != 7 ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_cs = uniform_rsrc(p.cscale, p.cscale ? FULL : 0u);
+            const unsigned o_px = e_ok ? (unsigned)(pix0 * ld + e_n - (first ? 0 : p.n0)) * 4u : LEAN_OOB;
+            const unsigned o_row = (unsigned)ld * 4u;
+            const unsigned o_cs = (unsigned)(b * p.cs_ld + e_n) * 4u;
+            f32x4 bv[4], sv[4], rv[4][2], mv[4][2], av[4][2];
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int n = e_n + 8 * g;
-                    const bool first = n < p.n0;
-                    float* dst = first ? p.dst0 : p.dst1;
-                    const float* msk = first ? p.mask0 : p.mask1;
-                    const int ld = first ? p.n0 : n1;
-                    const long long o0 = first ? r0 + n : r1 + (n - p.n0);
-                    f32x4 y[2] = {{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]},
-                                  {y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]}};
-                    const f32x4 bv = p.bias && PU_WF_ABL != 7 ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int g = 0; g < 4; ++g) {
+                bv[g] = epi_ld4(r_bias, (unsigned)(e_n + 8 * g) * 4u);
+                sv[g] = epi_ld4(r_cs, o_cs + 32u * g);
 #pragma unroll
-                    for (int o = 0; o < 2; ++o) {
-                        const long long off = o0 + o * ld;
-                        f32x4 v = y[o];
-                        if (p.bias) v += bv;
-                        if (p.resid) v += *reinterpret_cast<const f32x4*>(p.resid + off);
-                        if (relu) {
+                for (int o = 0; o < 2; ++o) {
+                    const unsigned off = o_px + o * o_row + 32u * g;
+                    rv[g][o] = epi_ld4(r_res, off);
+                    mv[g][o] = epi_ld4(r_msk, off);
+                    av[g][o] = epi_ld4(r_acc, off);
+                }
+            }
+            // pin every load here, ahead of the stores (the flag branches below would otherwise
+            // take them in, each load then waited for behind the stores before it)
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-                        }
-                        if (msk) {
-                            const f32x4 mv = *reinterpret_cast<const f32x4*>(msk + off);
+            for (int g = 0; g < 4; ++g) {
+                asm volatile("" :: "v"(bv[g]), "v"(sv[g]));
 #pragma unroll
-                            for (int e = 0; e < 4; ++e) if (!(mv[e] > 0.f)) v[e] = 0.f;
-                        }
-                        if (p.cscale) v *= *reinterpret_cast<const f32x4*>(p.cscale + (long long)b * p.cs_ld + n);
-                        if (accum) v += *reinterpret_cast<const f32x4*>(dst + off);
-                        if (PU_WF_ABL == 6) {      // no output stores (timing only): keep v alive
-                            if (v[0] == 1.2345e-30f) *reinterpret_cast<f32x4*>(dst + off) = v;
-                        } else {
-                            *reinterpret_cast<f32x4*>(dst + off) = v;
-                        }
+                for (int o = 0; o < 2; ++o) asm volatile("" :: "v"(rv[g][o]), "v"(mv[g][o]), "v"(av[g][o]));
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 y[2] = {{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]},
+                                    {y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]}};
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    f32x4 v = y[o];
+                    if (p.bias) v += bv[g];
+                    if (p.resid) v += rv[g][o];
+                    if (relu) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                    }
+                    if (msk) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) if (!(mv[g][o][e] > 0.f)) v[e] = 0.f;
+                    }
+                    if (p.cscale) v *= sv[g];
+                    if (accum) v += av[g][o];
+                    const unsigned off = o_px + o * o_row + 32u * g;
+                    if (PU_WF_ABL == 6) {      // no output stores (timing only): keep v alive
+                        if (v[0] == 1.2345e-30f) epi_st4(r_dst, off, v);
+                    } else {
+                        epi_st4(r_dst, off, v);
                     }
                 }
-            } else {
-                float* part = p.part + (long long)cur.kz * p.M * p.N + pix0 * p.N + e_n;
+            }
+        } else if (e_ok) {
+            float* part = p.part + (long long)cur.kz * p.M * p.N + pix0 * p.N + e_n;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    *reinterpret_cast<f32x4*>(part + 8 * g) = f32x4{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]};
-                    *reinterpret_cast<f32x4*>(part + p.N + 8 * g) = f32x4{y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]};
-                }
+            for (int g = 0; g < 4; ++g) {
+                *reinterpret_cast<f32x4*>(part + 8 * g) = f32x4{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]};
+                *reinterpret_cast<f32x4*>(part + p.N + 8 * g) = f32x4{y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]};
             }
         }
         if (!nxt.live) break;
@@ -602,6 +641,10 @@ bool wino_ok(const pu_conv_args* a, bool vec_epi) {
     const long long px = (long long)a->batch * a->in_h * a->in_w + a->in_w + 1;
     if (px * a->c0 * 4 >= (1LL << 31)) return false;
     if ((long long)C * a->n * 96 >= (1LL << 31)) return false;
+    // the epilogue's 32-bit destination offsets and item-uniform destination (64-channel items
+    // never straddle the split column n0)
+    if ((long long)a->batch * a->out_h * a->out_w * a->n * 4 >= (1LL << 31) - 64) return false;
+    if (a->n0 != a->n && a->n0 % WG_BN) return false;
     return ((uintptr_t)a->wino & 15) == 0;
 }
 
