@@ -12,6 +12,10 @@
 // channels of one pixel, stored as 8 bytes.
 #include "common.h"
 
+#ifndef PU_EPI_BATCH
+#define PU_EPI_BATCH 1   // 0: every output through epi_store4_b (A/B builds)
+#endif
+
 namespace pu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -99,6 +103,98 @@ __device__ __forceinline__ void epi_store4_b(const IgemmBf16Params& p, const Epi
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
     *reinterpret_cast<bf16x4*>(dst + off) = o;
+}
+
+// The two common epilogue forms - bias (+ReLU), the forward, or masks (+ReLU), the data gradient -
+// for an [NI][NJ] grid of 32 x 32 accumulator fragments, with every operand load issued before the
+// first store: gfx9's vmcnt counts stores too, so epi_store4_b's load-then-store per output made
+// each output wait out the previous stores' round trips (in the persistent halo kernel, right
+// before the next tile's first group).  Buffer descriptors with 32-bit offsets, wave-uniform per
+// 32-column fragment (n0 % 32 == 0); lanes past M / N load zeros and drop their stores.  Same
+// operations and rounding as epi_store4_b.  epi_batch_b_ok: the launch takes this form.
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t epi_rsrc_b(const void* base, bool on) {
+    const unsigned long long b = (unsigned long long)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(ub, 0, on ? 0x7fffffff : 0, 0x00020000);
+}
+
+__device__ __forceinline__ int epi_batch_b_ok(const IgemmBf16Params& p) {
+    if (PU_EPI_BATCH == 0 || (p.flags & (PU_EPI_SHUFFLE2 | PU_EPI_ACCUM)) || p.resid || p.n0 % 32 || p.N % 32 ||
+        (long long)p.M * p.N >= (1LL << 29))
+        return 0;
+    const bool mk = p.mask0 || p.mask1;
+    return mk && !p.bias ? 1 : (!mk && p.bias ? 2 : 0);     // 1 masks, 2 bias
+}
+
+template <bool MASK, int NI, int NJ>
+__device__ __forceinline__ void epilogue_batched_b(const IgemmBf16Params& p, f32x16 (&acc)[NI][NJ], int m0, int nc0,
+                                                   int lr, int lh) {
+    const bool relu = p.flags & PU_EPI_RELU;
+    const int n1 = p.N - p.n0;
+    unsigned orow[NI][NJ];             // byte offset of (row m, fragment column 0), LEAN_OOB past M / N
+    bool first[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) first[j] = nc0 + j * 32 < p.n0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int m = m0 + i * 32 + lr;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int c = nc0 + j * 32 + 4 * lh - (first[j] ? 0 : p.n0);
+            orow[i][j] = m < p.M && nc0 + j * 32 < p.N ? (unsigned)(m * (first[j] ? p.n0 : n1) + c) * 2u : LEAN_OOB;
+        }
+    }
+    u32x2_t mv[NI][NJ][4];             // MASK: 4 bf16 mask values per output
+    f32x4 bv[NJ][4];                   // !MASK: the bias of the output's channels
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        if constexpr (MASK) {
+            const __bf16* mk = first[j] ? p.mask0 : p.mask1;
+            const __amdgpu_buffer_rsrc_t r = epi_rsrc_b(mk, mk != nullptr);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) mv[i][j][q] = __builtin_amdgcn_raw_buffer_load_b64(r, orow[i][j], 16 * q, 0);
+        } else {
+            const __amdgpu_buffer_rsrc_t r = epi_rsrc_b(p.bias, true);
+            const unsigned nb = nc0 + j * 32 < p.N ? (unsigned)(nc0 + j * 32 + 4 * lh) * 4u : LEAN_OOB;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                bv[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, nb, 32 * q, 0));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const __amdgpu_buffer_rsrc_t rd = epi_rsrc_b(first[j] ? p.dst0 : p.dst1, true);
+        const bool has_mk = (first[j] ? p.mask0 : p.mask1) != nullptr;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                if constexpr (!MASK) v += bv[j][q];
+                if (relu) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                }
+                if constexpr (MASK) {
+                    if (has_mk) {
+                        const bf16x4 mb = __builtin_bit_cast(bf16x4, mv[i][j][q]);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) if (!((float)mb[e] > 0.f)) v[e] = 0.f;
+                    }
+                }
+                bf16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o), rd, orow[i][j], 16 * q, 0);
+            }
+    }
 }
 
 // the same epilogue for channels n..n+7 of pixel m (non-SHUFFLE2, n0 % 8 == 0): 16-byte loads and
@@ -521,6 +617,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         }
         return;
     }
+    if (const int eb = epi_batch_b_ok(p)) {
+        if (eb == 1) epilogue_batched_b<true>(p, acc, m_blk + wm * (BM / WM), n_blk + wn * (BN / WN), lr, lh);
+        else epilogue_batched_b<false>(p, acc, m_blk + wm * (BM / WM), n_blk + wn * (BN / WN), lr, lh);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
         const int m = m_blk + wm * (BM / WM) + i * 32 + lr;
@@ -698,20 +799,27 @@ __global__ __launch_bounds__(HB_NT) __attribute__((amdgpu_waves_per_eu(2))) void
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[kk][j], fx[kk][i], acc[i][j], 0, 0, 0);
             }
         }
+        const int eb = epi_batch_b_ok(p);
+        if (eb == 1) {
+            epilogue_batched_b<true>(p, acc, m_blk + p0, n_blk, lr, lh);
+        } else if (eb == 2) {
+            epilogue_batched_b<false>(p, acc, m_blk + p0, n_blk, lr, lh);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int m = m_blk + p0 + i * 32 + lr;
-            const EpiRowB er = epi_row_b(p, m);
+            for (int i = 0; i < 2; ++i) {
+                const int m = m_blk + p0 + i * 32 + lr;
+                const EpiRowB er = epi_row_b(p, m);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int n = n_blk + j * 32 + 8 * q + 4 * lh;
-                    f32x4 v;
+                    for (int q = 0; q < 4; ++q) {
+                        const int n = n_blk + j * 32 + 8 * q + 4 * lh;
+                        f32x4 v;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-                    epi_store4_b(p, er, n, v);
-                }
+                        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                        epi_store4_b(p, er, n, v);
+                    }
+            }
         }
         if (next >= t_end) break;
         tile = next;
