@@ -353,9 +353,17 @@ def main():
     roof = None
     if not args.no_kernel_profile:
         nprof = max(1, min(3, args.steps))
-        with K.KernelProfiler() as prof:
-            for i in range(nprof):
-                loss, hebb = trainer.step(xs[i % NB], ts[i % NB], hebb)
+        # one stream for this pass: with the bf16 trunk's weight-gradient side stream (timed region
+        # above) a launch's events would also time the kernels running beside it
+        from punet import trunk as _trunk
+        side = _trunk._SIDE
+        _trunk.set_side_stream(False)
+        try:
+            with K.KernelProfiler() as prof:
+                for i in range(nprof):
+                    loss, hebb = trainer.step(xs[i % NB], ts[i % NB], hebb)
+        finally:
+            _trunk.set_side_stream(side)
         summ = prof.summary()
         kern = {}
         for tag, d in sorted(summ.items(), key=lambda kv: -kv[1]["ms"]):
