@@ -238,11 +238,18 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
             raise RuntimeError("chan_scale must be [batch, channels]")
         a.chan_scale, a.chan_scale_ld = chan_scale.data_ptr(), chan_scale.shape[1]
     w6 = getattr(weight, "_split6", None) if (dt != BF16 and _FP32_MATH == "split6") else None
+    wn = getattr(weight, "_wino", None) if (w6 is not None and _WINO) else None
     if w6 is not None:
         a.weight6 = w6.data_ptr()
-        wn = getattr(weight, "_wino", None) if _WINO else None
-        if wn is not None:
-            a.wino = wn.data_ptr()
+    if wn is not None:
+        a.wino = wn.data_ptr()
+        # the signature wino_ok reads: shapes, flags, which operands exist, their alignment
+        key = (batch, tuple(in_hw), tuple(out_hw), k, stride, pad, c0, c1, n, a.n0, k_pad, cgroup, flags,
+               tuple(None if t is None else t.data_ptr() % 16
+                     for t in (src0, src1, bias, dst0, dst1, mask0, mask1, resid, chan_scale, weight, w6, wn)))
+        _ensure_direct(a, weight, key)
+    elif getattr(weight, "_direct_ok", True) is False:     # a direct call (e.g. Winograd switched off)
+        _refresh_direct(weight)
     L = lib()
     if dt == BF16:
         _igemm_bf16(L, a, batch, out_hw, k, c0, c1, n, dst0)
@@ -370,6 +377,10 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
             n, c = (d0, d1) if mode == 0 else (d1, d0)
             out._wino = torch.empty(lib().pu_wino_bytes(n, c) // 2, dtype=BF16, device=w.device)
             pack_wino([(w, out._wino, mode == 1)])
+            # the direct operand of a layer that only ever runs on Winograd is not refreshed after
+            # the optimizer step (trunk._Packs.refresh); igemm repacks it on the first call that
+            # takes the direct kernel (_ensure_direct)
+            out._src, out._direct_ok, out._wino_only = w, True, True
         elif hasattr(out, "_wino"):
             # a U packed from the old weights must not outlive them: repacked in place with
             # Winograd off, then Winograd back on, igemm would otherwise run on the stale U
@@ -378,10 +389,11 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
     return out
 
 
-def pack_weights(jobs):
+def pack_weights(jobs, wino=True):
     """Refresh many packed operands in one launch (pu_pack_weights).  jobs: (w, packed, planes) with
     ``packed`` an output of pack_weight (fp32 or bf16; its mode / k_pad / cgroup are read from the
-    attributes pack_weight stored on it) and ``planes`` its split6 planes or None."""
+    attributes pack_weight stored on it) and ``planes`` its split6 planes or None.  wino: also
+    refresh the Winograd operands the packed operands carry (one more launch)."""
     if not jobs:
         return
     arr = (PackJob * len(jobs))()
@@ -396,8 +408,36 @@ def pack_weights(jobs):
         nbytes += 4.0 * w.numel() + packed.element_size() * packed.numel() + (0 if planes is None else 2.0 * planes.numel())
     with _Rec("pack_weight", nbytes=nbytes):
         check(lib().pu_pack_weights(arr, len(jobs), _stream()), "pu_pack_weights")
-    pack_wino([(w, packed._wino, packed._pack_spec[0] == 1) for w, packed, _ in jobs
-               if getattr(packed, "_wino", None) is not None])
+    for _, packed, _ in jobs:
+        if hasattr(packed, "_direct_ok"):
+            packed._direct_ok = True
+    if wino:
+        pack_wino([(w, packed._wino, packed._pack_spec[0] == 1) for w, packed, _ in jobs
+                   if getattr(packed, "_wino", None) is not None])
+
+
+_WINO_TAKES = {}    # call signature -> does pu_conv_igemm take the Winograd kernel for it
+
+
+def _ensure_direct(a, weight, key):
+    """A Winograd-carrying operand on a call: if the library takes the direct kernel for this call
+    (pu_conv_igemm_tile's answer, cached per signature), refresh the direct operand if the last
+    repack skipped it, and keep refreshing it from now on."""
+    takes = _WINO_TAKES.get(key)
+    if takes is None:
+        bm, bn, mode, ks = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().pu_conv_igemm_tile(ctypes.byref(a), ctypes.byref(bm), ctypes.byref(bn), ctypes.byref(mode),
+                                       ctypes.byref(ks)), "pu_conv_igemm_tile")
+        takes = _WINO_TAKES[key] = mode.value == 6
+    if not takes:
+        weight._wino_only = False
+        if not weight._direct_ok:
+            _refresh_direct(weight)
+
+
+def _refresh_direct(weight):
+    weight._wino_only = False
+    pack_weights([(weight._src, weight, getattr(weight, "_split6", None))], wino=False)
 
 
 def split_weight6(packed):

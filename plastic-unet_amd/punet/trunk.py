@@ -35,6 +35,10 @@ from ._lib import PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PA
 _SIDE = {"1": True, "0": False}.get(os.environ.get("PU_WSTREAM", ""), "bf16")
 
 
+# PU_LAZY_DIRECT=0: refresh every packed direct operand after each optimizer step (A/B runs)
+_LAZY = os.environ.get("PU_LAZY_DIRECT", "1") != "0"
+
+
 def set_side_stream(on):
     """Switch the weight-gradient side stream for backward passes started after this call:
     True / False, or "bf16" (the default: bf16 trunks only)."""
@@ -68,8 +72,16 @@ class _Packs:
         stale = [(key, w, packed) for key, (ver, packed, w) in self.cache.items()
                  if w._version != ver and w.data_ptr() == key[0]]
         if stale:
-            K.pack_weights([(w.detach(), packed, getattr(packed, "_split6", None)) for _, w, packed in stale])
+            # operands only ever used by the Winograd kernel get their U refreshed, not the
+            # direct operand (K._ensure_direct repacks it if a call ever needs it)
+            direct = [(w.detach(), packed, getattr(packed, "_split6", None)) for _, w, packed in stale
+                      if not (_LAZY and getattr(packed, "_wino_only", False))]
+            K.pack_weights(direct, wino=False)
+            K.pack_wino([(w.detach(), packed._wino, packed._pack_spec[0] == 1) for _, w, packed in stale
+                         if getattr(packed, "_wino", None) is not None])
             for key, w, packed in stale:
+                if _LAZY and getattr(packed, "_wino_only", False):
+                    packed._direct_ok = False
                 self.cache[key] = (w._version, packed, w)
 
 

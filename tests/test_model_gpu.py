@@ -386,3 +386,38 @@ def test_c2_side_stream_weight_gradients_bitwise(precision):
     for k in res[0][2]:
         assert torch.equal(res[0][2][k], res[1][2][k]), k
     assert torch.equal(res[0][3], res[1][3])
+
+
+def test_lazy_direct_operands_after_optimizer_steps():
+    """After an optimizer step the trunk refreshes only the Winograd operand of a layer that has
+    only ever run on the Winograd kernel (trunk._Packs.refresh); a later call that takes the direct
+    kernel (here: Winograd switched off) must repack the direct operand first.  Compared bit for
+    bit with fresh models holding the same weights (they pack everything at first use)."""
+    from punet import kernels as K
+    from punet.engine import Trainer
+    torch.manual_seed(4)
+    net = UNetp(1, 1, DEV, rule="oja", nbf=64, depth=4, base_ch=32)
+    tr = Trainer(net, lr=1e-3, steplr=1e5)
+    g = torch.Generator().manual_seed(9)
+    hebb = (0.05 * torch.randn(2, 64, 64, generator=g)).to(DEV)
+    for _ in range(2):
+        x = torch.rand(2, 1, 64, 64, generator=g).to(DEV)
+        t = (torch.rand(2, 64, 64, generator=g) > 0.5).float().to(DEV)
+        _, hebb = tr.step(x, t, hebb)
+    x = torch.rand(2, 1, 64, 64, generator=g).to(DEV)
+    with torch.no_grad():
+        K.set_wino(False)
+        try:
+            y_direct, h_direct = net(x, hebb)
+            ref = UNetp(1, 1, DEV, rule="oja", nbf=64, depth=4, base_ch=32)
+            ref.load_state_dict(net.state_dict())
+            r_direct, rh_direct = ref(x, hebb)
+        finally:
+            K.set_wino(True)
+        y_wino, _ = net(x, hebb)
+        ref2 = UNetp(1, 1, DEV, rule="oja", nbf=64, depth=4, base_ch=32)
+        ref2.load_state_dict(net.state_dict())
+        r_wino, _ = ref2(x, hebb)
+    assert torch.equal(y_direct, r_direct) and torch.equal(h_direct, rh_direct)
+    assert torch.equal(y_wino, r_wino)
+    assert not torch.equal(y_direct, y_wino)      # the two paths really are different kernels
