@@ -101,8 +101,13 @@ int pu_device_info(int device, int* num_cu, int* clock_khz, long long* hbm_bytes
  * default and kept as an accepted no-op flag. */
 /* PU_CONV_NO_SMALLX6: a dispatch hint - keep an 8/16-channel 3x3 layer on the VALU direct kernel
  * instead of the 16x16x32 MFMA one (A/B runs) */
+/* PU_EPI_OUT_BF16: the single-channel stem conv only (c0 == 1, c1 == 0, 3x3 / s1 / p1 same size,
+ * n in {8, 16, 32, 64}, no mask / resid / ACCUM / SHUFFLE2 / chan_scale, n0 == n): dst0 is a bf16
+ * NHWC tensor and each fp32 result (after bias and ReLU) is rounded to bf16 once, to nearest even -
+ * what a separate fp32 -> bf16 conversion of the fp32 output would store (the bf16 trunk's stem,
+ * config C3).  Any other call with this flag fails with PU_ERR_INVALID. */
 enum { PU_EPI_RELU = 1, PU_EPI_ACCUM = 2, PU_EPI_SHUFFLE2 = 4, PU_EPI_RESID = 8, PU_CONV_NO_HALO = 16,
-       PU_CONV_HALO_V1 = 32, PU_CONV_NO_SMALLX6 = 64, PU_CONV_HALO_DMA = 128 };
+       PU_CONV_HALO_V1 = 32, PU_CONV_NO_SMALLX6 = 64, PU_CONV_HALO_DMA = 128, PU_EPI_OUT_BF16 = 256 };
 
 typedef struct {
     int batch;
@@ -192,7 +197,10 @@ typedef struct {
     float* dbias;
     int accumulate;
     /* fp32 GEMM arithmetic: 0 = v_mfma_f32_32x32x2_f32; 1 = each product as 6 exact bf16 products
-     * (hi/mid/lo split of both operands, fp32 accumulation) on v_mfma_f32_32x32x16_bf16 */
+     * (hi/mid/lo split of both operands, fp32 accumulation) on v_mfma_f32_32x32x16_bf16;
+     * 2 = the single-channel stem (c0 == 1, c1 == 0, 3x3 / s1 / p1 same size, n = 8, 16, 32 or 64,
+     * bias_mode 1) with `rows` a bf16 NHWC tensor: each bf16 dZ is widened exactly, so the result is
+     * bit-identical to math 1 on the widened fp32 copy (the bf16 trunk's stem, config C3) */
     int math;
 } pu_wgrad_args;
 

@@ -1184,7 +1184,9 @@ __global__ __launch_bounds__(256) void conv1x1_small_kernel(const IgemmParams p)
 // epilogue (bias, ReLU, masks, ...) stores 4 pixels x N channels contiguously.
 constexpr int ST_TH = 16, ST_TW = 64;
 
-template <int N>
+// BF16OUT (PU_EPI_OUT_BF16): bias + ReLU, then one round-to-nearest-even to bf16 and an 8-byte store
+// into a bf16 NHWC dst0 (the bf16 trunk's stem: no separate fp32 tensor and conversion pass)
+template <int N, bool BF16OUT = false>
 __global__ __launch_bounds__(256) void stem_conv_kernel(const IgemmParams p) {
     constexpr int L = N / 4;                  // lanes per pixel
     constexpr int PG = 256 / L;               // pixels per block pass
@@ -1224,7 +1226,20 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const IgemmParams p) {
             for (int e = 0; e < 4; ++e) v[e] = fmaf(a, w[t][e], v[e]);
         }
         const int m = (b * p.Ho + oy) * p.Wo + ox;
-        epi_store4(p, epi_row(p, m), 4 * lane_c, v);
+        if constexpr (BF16OUT) {
+            if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + 4 * lane_c);
+            if (p.flags & PU_EPI_RELU) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+            typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+            bf16x4_t o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+            *reinterpret_cast<bf16x4_t*>(reinterpret_cast<__bf16*>(p.dst0) + (long long)m * N + 4 * lane_c) = o;
+        } else {
+            epi_store4(p, epi_row(p, m), 4 * lane_c, v);
+        }
     }
 }
 
@@ -1456,6 +1471,19 @@ extern "C" int pu_conv_igemm(const pu_conv_args* a, void* stream) {
 
     hipStream_t s = as_stream(stream);
     const int N = a->n;
+    if (a->flags & PU_EPI_OUT_BF16) {
+        PU_REQUIRE(stem_conv_ok(a) && !a->mask0 && !a->mask1 && !a->resid && !a->chan_scale && a->n0 == a->n &&
+                       !(a->flags & (PU_EPI_ACCUM | PU_EPI_SHUFFLE2)) && ((uintptr_t)a->dst0 & 7) == 0,
+                   "pu_conv_igemm: PU_EPI_OUT_BF16 is the single-channel stem conv only (c0 1, 3x3/s1/p1, n 8/16/32/64, "
+                   "no mask/resid/accum/shuffle/chan_scale, 8-byte aligned dst0)");
+        p.ksplit = 1;
+        const dim3 sgrid((unsigned)(((a->out_w + ST_TW - 1) / ST_TW) * ((a->out_h + ST_TH - 1) / ST_TH) * a->batch));
+        if (N == 64) hipLaunchKernelGGL((stem_conv_kernel<64, true>), sgrid, dim3(256), 0, s, p);
+        else if (N == 32) hipLaunchKernelGGL((stem_conv_kernel<32, true>), sgrid, dim3(256), 0, s, p);
+        else if (N == 16) hipLaunchKernelGGL((stem_conv_kernel<16, true>), sgrid, dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((stem_conv_kernel<8, true>), sgrid, dim3(256), 0, s, p);
+        return check_launch("pu_conv_igemm (stem, bf16 out)");
+    }
     if (stem_conv_ok(a)) {
         p.ksplit = 1;
         const dim3 sgrid((unsigned)(((a->out_w + ST_TW - 1) / ST_TW) * ((a->out_h + ST_TH - 1) / ST_TH) * a->batch));

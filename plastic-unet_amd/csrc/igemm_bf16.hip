@@ -1397,6 +1397,7 @@ static int setup_bf16(const pu_conv_args* a, IgemmBf16Params* pp, long long* Mou
     PU_REQUIRE(a->kh > 0 && a->kw > 0 && a->stride > 0 && a->pad >= 0 && a->kh * a->kw <= 32, "pu_conv_igemm_bf16: bad taps");
     PU_REQUIRE(a->src0 && a->weight && a->dst0 && a->n > 0, "pu_conv_igemm_bf16: operands");
     PU_REQUIRE(a->chan_scale == nullptr, "pu_conv_igemm_bf16: chan_scale is an fp32-path epilogue");
+    PU_REQUIRE(!(a->flags & PU_EPI_OUT_BF16), "pu_conv_igemm_bf16: PU_EPI_OUT_BF16 is pu_conv_igemm's stem flag");
     PU_REQUIRE(a->c0 % 32 == 0 && a->c1 % 32 == 0 && a->c0 > 0 && (a->c1 == 0 || a->src1),
                "pu_conv_igemm_bf16: channel counts (%d, %d) must be multiples of 32", a->c0, a->c1);
     PU_REQUIRE(a->cgroup == 0 || a->cgroup == 32, "pu_conv_igemm_bf16: cgroup must be 0 or 32");

@@ -1171,7 +1171,9 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
 // finishes - deterministic like every other weight gradient.
 constexpr int SWS_TH = 16, SWS_TW = 64;
 
-template <int N>
+// BF16ROWS (pu_wgrad_args.math == 2): dZ is a bf16 NHWC tensor, widened exactly on load (the bf16
+// trunk's stem: no fp32 copy of dZ), otherwise the same fmaf chains
+template <int N, bool BF16ROWS = false>
 __global__ __launch_bounds__(256) void wgrad_stem_kernel(const WgradParams p) {
     constexpr int L = N / 4, PG = 256 / L;
     constexpr int HH = SWS_TH + 2, HW = SWS_TW + 2;
@@ -1204,7 +1206,15 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(const WgradParams p) {
             const int oy = tyi * SWS_TH + row, ox = txi * SWS_TW + col;
             if (oy >= p.Ho || ox >= p.Wo) continue;
             const long long m = ((long long)b * p.Ho + oy) * p.Wo + ox;
-            const f32x4 dz = *reinterpret_cast<const f32x4*>(p.P + m * N + 4 * lane_c);
+            f32x4 dz;
+            if constexpr (BF16ROWS) {
+                typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+                const bf16x4_t zb = *reinterpret_cast<const bf16x4_t*>(reinterpret_cast<const __bf16*>(p.P) + m * N + 4 * lane_c);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dz[e] = (float)zb[e];
+            } else {
+                dz = *reinterpret_cast<const f32x4*>(p.P + m * N + 4 * lane_c);
+            }
 #pragma unroll
             for (int t9 = 0; t9 < 9; ++t9) {
                 const float a = smem[(row + t9 / 3) * HW + col + t9 % 3];
@@ -1838,6 +1848,8 @@ static int plan_wgrad(const pu_wgrad_args* a, WgradPlan* pl) {
     PU_REQUIRE(a->bias_mode >= 0 && a->bias_mode <= 2, "pu_wgrad: bias_mode");
     PU_REQUIRE(a->bias_mode == 0 || a->dbias, "pu_wgrad: dbias missing");
     PU_REQUIRE(a->dweight, "pu_wgrad: dweight missing");
+    PU_REQUIRE(a->math >= 0 && a->math <= 2, "pu_wgrad: math %d", a->math);
+    PU_REQUIRE(a->math != 2 || stem_wgrad_ok(a), "pu_wgrad: math 2 (bf16 rows) is the single-channel stem only");
     const long long M = (long long)a->batch * a->out_h * a->out_w;
     PU_REQUIRE(M < (1LL << 31), "pu_wgrad: too many pixels");
     pl->M = (int)M;
@@ -2584,6 +2596,15 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
     p.gx = pl.gx;
     p.gy = pl.gy;
     p.batch = a->batch; p.tiles_w = pl.tiles_w; p.tiles_h = pl.tiles_h;
+    if (pl.stem && (phase & 1) && a->math == 2) {
+        if (a->n == 64) hipLaunchKernelGGL((wgrad_stem_kernel<64, true>), dim3(pl.splits), dim3(256), 0, s, p);
+        else if (a->n == 32) hipLaunchKernelGGL((wgrad_stem_kernel<32, true>), dim3(pl.splits), dim3(256), 0, s, p);
+        else if (a->n == 16) hipLaunchKernelGGL((wgrad_stem_kernel<16, true>), dim3(pl.splits), dim3(256), 0, s, p);
+        else hipLaunchKernelGGL((wgrad_stem_kernel<8, true>), dim3(pl.splits), dim3(256), 0, s, p);
+        st = check_launch("pu_wgrad (stem, bf16 rows)");
+        if (st != PU_OK) return st;
+        phase &= ~1;
+    }
     if (pl.stem && (phase & 1)) {
         if (a->n == 64) hipLaunchKernelGGL(wgrad_stem_kernel<64>, dim3(pl.splits), dim3(256), 0, s, p);
         else if (a->n == 32) hipLaunchKernelGGL(wgrad_stem_kernel<32>, dim3(pl.splits), dim3(256), 0, s, p);

@@ -18,7 +18,7 @@ c_double = ctypes.c_double
 P = ctypes.c_void_p
 
 (PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1, PU_CONV_NO_SMALLX6,
- PU_CONV_HALO_DMA) = 1, 2, 4, 8, 16, 32, 64, 128
+ PU_CONV_HALO_DMA, PU_EPI_OUT_BF16) = 1, 2, 4, 8, 16, 32, 64, 128, 256
 PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PACK_CONVT_DGRAD, PU_PACK_CONVT3_FWD = 0, 1, 2, 3, 4
 PU_RULE_HEBB, PU_RULE_OJA = 0, 1
 

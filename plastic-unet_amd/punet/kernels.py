@@ -11,7 +11,7 @@ import torch
 from . import _lib
 from ._lib import (ConvArgs, WgradArgs, PlasticArgs, PlasticHeadArgs, PlasticBwdArgs, AdamTensor, PackJob, WinoJob, check,
                    PU_EPI_RELU, PU_EPI_ACCUM, PU_EPI_SHUFFLE2, PU_EPI_RESID, PU_CONV_NO_HALO, PU_CONV_HALO_V1, PU_CONV_HALO_DMA,
-                   PU_CONV_NO_SMALLX6)
+                   PU_CONV_NO_SMALLX6, PU_EPI_OUT_BF16)
 
 __all__ = ["KernelProfiler", "igemm", "wgrad", "pack_weight", "nchw_to_nhwc", "maxpool2_fwd", "maxpool2_bwd",
            "outconv_fwd", "outconv_bwd", "plastic_fwd", "trace_update", "plastic_bwd", "bce_fwd",
@@ -220,15 +220,18 @@ def igemm(*, batch, in_hw, out_hw, k, stride, pad, src0, c0, weight, k_pad, n, d
     """pu_conv_igemm: implicit-GEMM conv (3x3 fwd/dgrad, ConvT fwd with shuffle, ConvT dgrad).
     resid: residual tensor added before ReLU/mask; shuf = (out_h, out_w, crop) of a SHUFFLE2 grid;
     chan_scale: [batch, ld] per-(image, column) factors applied after the mask (the Dropout2d scale
-    of the tensor being produced; SHUFFLE2: per output channel)."""
+    of the tensor being produced; SHUFFLE2: per output channel).  A bf16 dst0 with fp32 operands
+    is the single-channel stem writing the bf16 trunk's first activation (PU_EPI_OUT_BF16)."""
     dt = _act_dtype(src0)
+    out_bf16 = dt == torch.float32 and dst0 is not None and dst0.dtype == BF16
     for t, nm in ((src0, "src0"), (src1, "src1"), (weight, "weight"), (dst0, "dst0"),
                   (dst1, "dst1"), (mask0, "mask0"), (mask1, "mask1"), (resid, "resid")):
-        _req(t, nm, dt)
+        _req(t, nm, BF16 if (out_bf16 and nm == "dst0") else dt)
     _req(bias, "bias")
     _req(chan_scale, "chan_scale")
     flags = (PU_EPI_RELU if relu else 0) | (PU_EPI_ACCUM if accum else 0) | (PU_EPI_SHUFFLE2 if shuffle else 0) \
-        | (PU_EPI_RESID if resid is not None else 0) | _halo_flags() | (0 if _SMALLX6 else PU_CONV_NO_SMALLX6)
+        | (PU_EPI_RESID if resid is not None else 0) | _halo_flags() | (0 if _SMALLX6 else PU_CONV_NO_SMALLX6) \
+        | (PU_EPI_OUT_BF16 if out_bf16 else 0)
     a = ConvArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                  _p(src0), c0, _p(src1), c1, _p(weight), k_pad, cgroup, n, _p(bias),
                  _p(dst0), n if n0 is None else n0, _p(dst1), _p(mask0), _p(mask1), flags, None, 0,
@@ -300,13 +303,15 @@ def wgrad(*, batch, in_hw, out_hw, k, stride, pad, rows, n, src0, c0, dweight, s
           bias_mode=0, dbias=None, accumulate=False):
     """pu_wgrad: split-K weight (+bias) gradient into PyTorch's [n][c][k][k] layout (fp32, or
     bf16 rows/sources with fp32 gradients)."""
-    dt = _act_dtype(rows)
+    # bf16 dZ with an fp32 single-channel source: the bf16 trunk's stem (pu_wgrad math 2)
+    stem_bf16 = rows.dtype == BF16 and src0.dtype == torch.float32 and c0 == 1 and src1 is None
+    dt = torch.float32 if stem_bf16 else _act_dtype(rows)
     for t, nm in ((rows, "rows"), (src0, "src0"), (src1, "src1")):
-        _req(t, nm, dt)
+        _req(t, nm, BF16 if (stem_bf16 and nm == "rows") else dt)
     _req(dweight, "dweight"); _req(dbias, "dbias")
     a = WgradArgs(batch, in_hw[0], in_hw[1], out_hw[0], out_hw[1], k, k, stride, pad,
                   _p(rows), n, _p(src0), c0, _p(src1), c1, bias_mode, _p(dweight), _p(dbias),
-                  1 if accumulate else 0, 1 if (dt != BF16 and _FP32_MATH == "split6") else 0)
+                  1 if accumulate else 0, 2 if stem_bf16 else (1 if (dt != BF16 and _FP32_MATH == "split6") else 0))
     L = lib()
     if dt == BF16:
         nbytes = L.pu_wgrad_bf16_workspace_bytes(ctypes.byref(a))

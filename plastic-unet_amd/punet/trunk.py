@@ -35,6 +35,8 @@ from ._lib import PU_PACK_CONV_FWD, PU_PACK_CONV_DGRAD, PU_PACK_CONVT_FWD, PU_PA
 _SIDE = {"1": True, "0": False}.get(os.environ.get("PU_WSTREAM", ""), "bf16")
 
 
+# PU_STEM_BF16=0: the bf16 trunk's stem writes fp32 and converts (A/B runs)
+_STEM_BF16 = os.environ.get("PU_STEM_BF16", "1") != "0"
 # PU_LAZY_DIRECT=0: refresh every packed direct operand after each optimizer step (A/B runs)
 _LAZY = os.environ.get("PU_LAZY_DIRECT", "1") != "0"
 
@@ -113,15 +115,16 @@ def _cg(dt, c0, c1=0):
     return 32
 
 
-def conv3x3(x0, w, b, packs, x1=None, relu=True):
-    """3x3/p1 conv (+bias, ReLU) over the channel concat [x0 | x1] (NHWC)."""
+def conv3x3(x0, w, b, packs, x1=None, relu=True, out_dtype=None):
+    """3x3/p1 conv (+bias, ReLU) over the channel concat [x0 | x1] (NHWC).  out_dtype bf16 with an
+    fp32 single-channel x0: the stem writes the bf16 trunk's first activation directly."""
     B, H, W, c0 = x0.shape
     c1 = 0 if x1 is None else x1.shape[3]
     cout = w.shape[0]
     dt = x0.dtype
     k_pad = _kp(9 * (c0 + c1), dt)
     g = _cg(dt, c0, c1)
-    out = torch.empty(B, H, W, cout, dtype=dt, device=x0.device)
+    out = torch.empty(B, H, W, cout, dtype=out_dtype or dt, device=x0.device)
     K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=x0, c0=c0, src1=x1, c1=c1,
             weight=packs.get(w, PU_PACK_CONV_FWD, k_pad, g, dt), k_pad=k_pad, n=cout, bias=b, dst0=out, relu=relu,
             cgroup=g)
@@ -286,6 +289,13 @@ class UNetpTrunk:
         self._ws = None          # weight-gradient side stream (PU_WSTREAM), created on first use
         self._side = None        # the side stream while a backward runs with it, else None
 
+    def _stem_bf16(self, x):
+        """bf16 trunk whose first conv is the single-channel stem (no BatchNorm): it writes its bf16
+        output directly (PU_EPI_OUT_BF16) and its weight gradient reads the bf16 dZ (pu_wgrad math
+        2) - no fp32 copies and conversion passes."""
+        return (_STEM_BF16 and self.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[3] == 1 and "inc.c0" not in self.bn
+                and self.params[self.slot["inc.c0"]].shape[0] in (8, 16, 32, 64))
+
     def backward_order(self):
         """Parameters in the order backward() completes their gradients (outc first, stem last;
         each BatchNorm pair completes just before its conv)."""
@@ -348,12 +358,12 @@ class UNetpTrunk:
         return _grad_sinks(self, self.slot["outc"])
 
     # -------------------------------------------------------------------------------- forward
-    def _conv(self, key, P, s, x0, x1=None):
+    def _conv(self, key, P, s, x0, x1=None, out_dtype=None):
         """conv3x3 (+ BatchNorm) + ReLU of conv `key` over [x0 | x1]."""
         i = self.slot[key]
         bnm = self.bn.get(key)
         if bnm is None:
-            return conv3x3(x0, P[i], P[i + 1], self.packs, x1=x1)
+            return conv3x3(x0, P[i], P[i + 1], self.packs, x1=x1, out_dtype=out_dtype)
         z = conv3x3(x0, P[i], P[i + 1], self.packs, x1=x1, relu=False)
         j = self.slot[key + ".bn"]
         training = self.training or not bnm.track_running_stats
@@ -383,7 +393,7 @@ class UNetpTrunk:
                     weight=pk.get(cw, PU_PACK_CONV_FWD, K.round16(ca)), k_pad=K.round16(ca), n=cw.shape[0],
                     bias=cb, dst0=x, relu=True)
             s["stem"] = x
-        t = self._conv("inc.c0", P, s, x)
+        t = self._conv("inc.c0", P, s, x, out_dtype=torch.bfloat16 if self._stem_bf16(x) else None)
         if self.dtype != t.dtype:
             t = K.to_bf16(t)
         s["inc.t"] = t
@@ -525,7 +535,7 @@ class UNetpTrunk:
         grads[c1], grads[c1 + 1] = self._wgrad(lambda o: conv3x3_wgrad(g, t, out=o), c1, out(c1), g, t)
         dt, _ = conv3x3_dgrad(g, P[c1], pk, mask0=t)
         x0 = s["stem"] if self.coord is not None else s["x"]
-        if dt.dtype != x0.dtype:       # bf16 trunk: the fp32 stem's weight gradient
+        if dt.dtype != x0.dtype and not self._stem_bf16(x0):   # bf16 trunk: the fp32 stem's weight gradient
             dt = K.to_f32(dt)
         dt = self._bn_back("inc.c0", dt, s, P, grads, out)
         grads[c0], grads[c0 + 1] = self._wgrad(lambda o: conv3x3_wgrad(dt, x0, out=o), c0, out(c0), dt, x0)

@@ -313,3 +313,38 @@ def test_bf16_halo2_conv_matches_fp32_and_halo1(B, H, c0, c1, cout):
     xc = torch.cat([x0, x1], 3) if c1 else x0
     ref = torch.relu(F.conv2d(nchw(xc.float()), rb(w), b, padding=1))
     close_bf16(nchw(outs[0][0]), ref)
+
+
+def test_bf16_stem_direct_output_and_bf16_rows_wgrad_bitwise():
+    """The bf16 trunk's single-channel stem writes its bf16 output directly (PU_EPI_OUT_BF16) and
+    its weight gradient reads the bf16 dZ (pu_wgrad math 2): bit for bit what the fp32 output +
+    conversion pass and the converted fp32 dZ gave (round-to-nearest-even once; bf16 -> fp32 is
+    exact).  Full model forward + backward both ways, then the flag's misuse fails loudly."""
+    res = []
+    for fused in (True, False):
+        orig = T.UNetpTrunk._stem_bf16
+        if not fused:
+            T.UNetpTrunk._stem_bf16 = lambda self, x: False
+        try:
+            torch.manual_seed(3)
+            net = UNetp(1, 1, DEV, rule="oja", nbf=64, depth=4, base_ch=32, precision="bf16")
+            g = torch.Generator().manual_seed(8)
+            x = torch.rand(4, 1, 64, 64, generator=g).to(DEV)
+            t = (torch.rand(4, 64, 64, generator=g) > 0.5).float().to(DEV)
+            H = (0.05 * torch.randn(4, 64, 64, generator=g)).to(DEV)
+            y, hn = net(x, H)
+            bce_loss(y, t).backward()
+            res.append((y.detach(), hn.detach(), {k: p.grad.detach().clone() for k, p in net.named_parameters()
+                                                  if p.grad is not None}))
+        finally:
+            T.UNetpTrunk._stem_bf16 = orig
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
+    # PU_EPI_OUT_BF16 on anything but the single-channel stem is an argument error
+    x = torch.rand(1, 8, 8, 16, device=DEV)
+    w = torch.randn(16, 16, 3, 3, device=DEV)
+    pk = K.pack_weight(w, 0, 16 * 9)
+    with pytest.raises(RuntimeError, match="PU_EPI_OUT_BF16"):
+        K.igemm(batch=1, in_hw=(8, 8), out_hw=(8, 8), k=3, stride=1, pad=1, src0=x, c0=16, weight=pk, k_pad=16 * 9,
+                n=16, dst0=torch.empty(1, 8, 8, 16, dtype=torch.bfloat16, device=DEV), relu=True)
