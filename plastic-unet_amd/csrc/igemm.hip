@@ -150,6 +150,62 @@ __device__ __forceinline__ void epilogue_batched(const IgemmParams& p, f32x16 (&
     }
 }
 
+// The ConvTranspose2d 2x2 / s2 forward's epilogue (SHUFFLE2 without a crop: column n = ij * co + c
+// goes to pixel (2ho + i, 2wo + j) of the 2H x 2W grid, + bias[c]) in the same batched form: every
+// bias load before the first store.  co % 32 == 0, so a 32-column fragment lies in one (i, j).
+template <int FM, int FN>
+__device__ __forceinline__ void epilogue_batched_shuf(const IgemmParams& p, f32x16 (&acc)[FM][FN], int m0, int nc0,
+                                                      int lr, int lh) {
+    const bool relu = p.flags & PU_EPI_RELU;
+    const int co = p.N >> 2;
+    unsigned orow[FM][FN];
+    int cj[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+        const int nj = nc0 + j * 32;
+        const int ij = nj < p.N ? nj / co : 0;
+        cj[j] = nj - ij * co + 4 * lh;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+            const int m = m0 + i * 32 + lr;
+            unsigned o = LEAN_OOB;
+            if (m < p.M && nj < p.N) {
+                const int t2 = fdiv(m, p.dWo);
+                const int wo = m - t2 * p.Wo;
+                const int bb = fdiv(t2, p.dHo);
+                const int ho = t2 - bb * p.Ho;
+                const int pix = (bb * p.shuf_h + 2 * ho + (ij >> 1)) * p.shuf_w + 2 * wo + (ij & 1);
+                o = (unsigned)(pix * co + cj[j]) * 4u;
+            }
+            orow[i][j] = o;
+        }
+    }
+    f32x4 bv[FN][4];
+    const __amdgpu_buffer_rsrc_t rb = epi_rsrc(p.bias, true);
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            bv[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)cj[j] * 4u, 32 * q, 0));
+    const __amdgpu_buffer_rsrc_t rd = epi_rsrc(p.dst0, true);
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                v += bv[j][q];
+                if (relu) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rd, orow[i][j], 32 * q, 0);
+            }
+}
+
 template <int BM, int BN, int WM, int WN, bool BATCH = false>
 __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM / WM / 32][BN / WN / 32], int m_blk,
                                          int n_blk, int wm, int wn, int lr, int lh) {
@@ -168,6 +224,12 @@ __device__ __forceinline__ void epilogue(const IgemmParams& p, f32x16 (&acc)[BM 
                 epilogue_batched<false, FM, FN>(p, acc, m0, nc0, lr, lh);
                 return;
             }
+        }
+        if (p.vec_epi && (p.flags & PU_EPI_SHUFFLE2) && !(p.flags & PU_EPI_ACCUM) && !p.resid && !p.cscale && p.bias &&
+            !p.mask0 && p.shuf_off == 0 && p.shuf_h == 2 * p.Ho && p.shuf_w == 2 * p.Wo && (p.N / 4) % 32 == 0 &&
+            p.N % 128 == 0 && (long long)p.M * p.N < (1LL << 29)) {
+            epilogue_batched_shuf<FM, FN>(p, acc, m_blk + wm * (BM / WM), n_blk + wn * (BN / WN), lr, lh);
+            return;
         }
     }
     // ---- epilogue.  acc[i][j] = D^T block: MFMA row = channel n = 8*(r>>2) + 4*(lane>>5) + (r&3),
