@@ -197,6 +197,71 @@ __device__ __forceinline__ void epilogue_batched_b(const IgemmBf16Params& p, f32
     }
 }
 
+// The ConvTranspose2d 2x2 / s2 forward (SHUFFLE2, no crop, bias, co % 32 == 0) in the batched form:
+// every bias load before the first store (the per-output epi_store4_b waited out each previous
+// store's round trip before its bias load).  Same operations and rounding as epi_store4_b.
+__device__ __forceinline__ bool epi_shuf_b_ok(const IgemmBf16Params& p) {
+    return PU_EPI_BATCH && (p.flags & PU_EPI_SHUFFLE2) && !(p.flags & PU_EPI_ACCUM) && !p.resid && p.bias && !p.mask0 &&
+           p.shuf_off == 0 && p.shuf_h == 2 * p.Ho && p.shuf_w == 2 * p.Wo && (p.N / 4) % 32 == 0 && p.N % 128 == 0 &&
+           (long long)p.M * p.N < (1LL << 29);
+}
+
+template <int NI, int NJ>
+__device__ __forceinline__ void epilogue_batched_shuf_b(const IgemmBf16Params& p, f32x16 (&acc)[NI][NJ], int m0,
+                                                        int nc0, int lr, int lh) {
+    const bool relu = p.flags & PU_EPI_RELU;
+    const int co = p.N >> 2;
+    unsigned orow[NI][NJ];
+    int cj[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int nj = nc0 + j * 32;
+        const int ij = nj < p.N ? nj / co : 0;
+        cj[j] = nj - ij * co + 4 * lh;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int m = m0 + i * 32 + lr;
+            unsigned o = LEAN_OOB;
+            if (m < p.M && nj < p.N) {
+                const int t2 = fdiv(m, p.dWo);
+                const int wo = m - t2 * p.Wo;
+                const int bb = fdiv(t2, p.dHo);
+                const int ho = t2 - bb * p.Ho;
+                const int pix = (bb * p.shuf_h + 2 * ho + (ij >> 1)) * p.shuf_w + 2 * wo + (ij & 1);
+                o = (unsigned)(pix * co + cj[j]) * 2u;
+            }
+            orow[i][j] = o;
+        }
+    }
+    f32x4 bv[NJ][4];
+    const __amdgpu_buffer_rsrc_t rb = epi_rsrc_b(p.bias, true);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            bv[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)cj[j] * 4u, 32 * q, 0));
+    const __amdgpu_buffer_rsrc_t rd = epi_rsrc_b(p.dst0, true);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f32x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+                v += bv[j][q];
+                if (relu) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                }
+                bf16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o), rd, orow[i][j], 16 * q, 0);
+            }
+}
+
 // the same epilogue for channels n..n+7 of pixel m (non-SHUFFLE2, n0 % 8 == 0): 16-byte loads and
 // stores, so 8 lanes cover a 64-channel pixel row of 128 contiguous bytes.  bias: preloaded.
 // Every lane issues the same memory operations (a lane whose destination has no mask still loads,
@@ -424,6 +489,10 @@ __global__ __launch_bounds__(256) void igemm_bf16_kernel(const IgemmBf16Params p
                     *reinterpret_cast<f32x4*>(part + (long long)m * p.N + n) = v;
                 }
         }
+        return;
+    }
+    if (epi_shuf_b_ok(p)) {
+        epilogue_batched_shuf_b(p, acc, m_blk + wm * (BM / WM), n_blk + wn * (BN / WN), lr, lh);
         return;
     }
 #pragma unroll
