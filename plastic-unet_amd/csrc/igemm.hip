@@ -1275,6 +1275,11 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const IgemmParams p) {
     for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int t = 0; t < 9; ++t) w[t][e] = p.wt[(long long)(4 * lane_c + e) * p.k_pad + t];
+    // bias (+ReLU) into one destination, the forward's form: the bias loaded once, ahead of the
+    // stores (epi_store4 reloads it per pixel, after the previous pixel's store - and vmcnt counts
+    // that store too)
+    const bool plain = !(p.flags & (PU_EPI_SHUFFLE2 | PU_EPI_ACCUM)) && !p.mask0 && !p.resid && !p.cscale && p.n0 == N;
+    const f32x4 bias4 = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + 4 * lane_c) : f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();
     for (int q = threadIdx.x / L; q < ST_TH * ST_TW; q += PG) {
         const int row = q / ST_TW, col = q - row * ST_TW;
@@ -1289,7 +1294,7 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const IgemmParams p) {
         }
         const int m = (b * p.Ho + oy) * p.Wo + ox;
         if constexpr (BF16OUT) {
-            if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + 4 * lane_c);
+            if (p.bias) v += bias4;
             if (p.flags & PU_EPI_RELU) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -1299,6 +1304,13 @@ __global__ __launch_bounds__(256) void stem_conv_kernel(const IgemmParams p) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (__bf16)v[e];
             *reinterpret_cast<bf16x4_t*>(reinterpret_cast<__bf16*>(p.dst0) + (long long)m * N + 4 * lane_c) = o;
+        } else if (plain) {
+            if (p.bias) v += bias4;
+            if (p.flags & PU_EPI_RELU) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+            *reinterpret_cast<f32x4*>(p.dst0 + (long long)m * N + 4 * lane_c) = v;
         } else {
             epi_store4(p, epi_row(p, m), 4 * lane_c, v);
         }
