@@ -1201,28 +1201,43 @@ __global__ __launch_bounds__(256) void wgrad_stem_kernel(const WgradParams p) {
                           ? p.src0[img + (long long)gy * p.Wi + gx] : 0.f;
         }
         __syncthreads();
-        for (int q = grp; q < SWS_TH * SWS_TW; q += PG) {
-            const int row = q / SWS_TW, col = q - row * SWS_TW;
-            const int oy = tyi * SWS_TH + row, ox = txi * SWS_TW + col;
-            if (oy >= p.Ho || ox >= p.Wo) continue;
-            const long long m = ((long long)b * p.Ho + oy) * p.Wo + ox;
-            f32x4 dz;
-            if constexpr (BF16ROWS) {
-                typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-                const bf16x4_t zb = *reinterpret_cast<const bf16x4_t*>(reinterpret_cast<const __bf16*>(p.P) + m * N + 4 * lane_c);
+        // 4 pixels per pass, their dZ loads issued together (unconditional: a pixel past the image
+        // edge loads pixel 0 and adds nothing), so the loop waits once per 4 loads
+        static_assert((SWS_TH * SWS_TW) % (4 * PG) == 0, "stem wgrad pass");
+        for (int q0 = grp; q0 < SWS_TH * SWS_TW; q0 += 4 * PG) {
+            f32x4 dzs[4];
+            bool ok[4];
+            int hb[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) dz[e] = (float)zb[e];
-            } else {
-                dz = *reinterpret_cast<const f32x4*>(p.P + m * N + 4 * lane_c);
+            for (int u = 0; u < 4; ++u) {
+                const int q = q0 + u * PG;
+                const int row = q / SWS_TW, col = q - row * SWS_TW;
+                const int oy = tyi * SWS_TH + row, ox = txi * SWS_TW + col;
+                ok[u] = oy < p.Ho && ox < p.Wo;
+                hb[u] = row * HW + col;
+                const long long m = ok[u] ? ((long long)b * p.Ho + oy) * p.Wo + ox : 0;
+                if constexpr (BF16ROWS) {
+                    typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+                    const bf16x4_t zb = *reinterpret_cast<const bf16x4_t*>(reinterpret_cast<const __bf16*>(p.P) + m * N + 4 * lane_c);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) dzs[u][e] = (float)zb[e];
+                } else {
+                    dzs[u] = *reinterpret_cast<const f32x4*>(p.P + m * N + 4 * lane_c);
+                }
             }
 #pragma unroll
-            for (int t9 = 0; t9 < 9; ++t9) {
-                const float a = smem[(row + t9 / 3) * HW + col + t9 % 3];
+            for (int u = 0; u < 4; ++u) {
+                if (!ok[u]) continue;
+                const f32x4 dz = dzs[u];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) acc[t9][e] = fmaf(a, dz[e], acc[t9][e]);
+                for (int t9 = 0; t9 < 9; ++t9) {
+                    const float a = smem[hb[u] + (t9 / 3) * HW + t9 % 3];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[t9][e] = fmaf(a, dz[e], acc[t9][e]);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[9][e] += dz[e];
             }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[9][e] += dz[e];
         }
     }
     __syncthreads();
