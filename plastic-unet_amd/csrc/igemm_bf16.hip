@@ -1440,6 +1440,14 @@ static bool lean128_on() {
     return on;
 }
 
+static bool smallm_on() {             // PU_BF16_SMALLM=0: the 256 x 128 split (A/B runs)
+    static const bool on = [] {
+        const char* e = getenv("PU_BF16_SMALLM");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static void plan_lean_b(const pu_conv_args* a, long long M, int* bm, int* bn, int* ksplit, int* t_per) {
     *bm = 256;
     *bn = a->n > 64 ? 128 : 64;
@@ -1449,8 +1457,22 @@ static void plan_lean_b(const pu_conv_args* a, long long M, int* bm, int* bn, in
     const int tiles = blocks_for_b(M, a->n, *bm, *bn);
     const int target = 512;
     if (tiles >= target - target / 16) return;
-    if (lean128_on() && a->n > 64 && blocks_for_b(M, a->n, 128, 128) >= 240) {
+    const int t128 = blocks_for_b(M, a->n, 128, 128);
+    if (lean128_on() && a->n > 64 && t128 >= 240) {
         *bm = 128;
+        return;
+    }
+    // small pixel grids (the 8^2 / 16^2 levels): 128 x 128 tiles split to ~2 blocks per CU.  The
+    // 256 x 128 tiles split 8 / 16 ways wrote 8 - 16 fp32 partial tiles per output (67 MB per 8^2
+    // layer, read back by the split epilogue) for blocks that ran 1 - 2 channel groups each
+    if (smallm_on() && a->n > 64) {
+        int k2 = ceil_div(target, t128);
+        if (k2 > T / 9) k2 = T / 9;
+        *bm = 128;
+        if (k2 >= 2) {
+            *t_per = ceil_div(ceil_div(T, k2), 9) * 9;
+            *ksplit = ceil_div(T, *t_per);
+        }
         return;
     }
     int ks = ceil_div(target, tiles);
