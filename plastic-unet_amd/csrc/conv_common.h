@@ -136,6 +136,7 @@ __device__ __forceinline__ void split3_pairs(const f32x4 lo4, const f32x4 hi4, b
 bool wino_ok(const pu_conv_args* a, bool vec_epi);
 size_t wino_workspace_bytes(const pu_conv_args* a);
 int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s);   // returns its K splits
+int wino_item_channels(const pu_conv_args* a);   // output channels per Winograd item (64 or 128)
 // 8/16-channel 3x3 convolutions on 16x16x32 bf16 MFMAs (smallconv.hip)
 bool smallx6_ok(const pu_conv_args* a, bool vec_epi);
 int smallx6_launch(const pu_conv_args* a, const IgemmParams& p, hipStream_t s);

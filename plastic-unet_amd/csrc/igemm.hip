@@ -1715,9 +1715,10 @@ extern "C" int pu_conv_igemm_tile(const pu_conv_args* a, int* bm, int* bn, int* 
         if (ksplit) *ksplit = 1;
         return PU_OK;
     }
-    if (wino_ok(a, vec_epilogue(a))) {  // reported as mode 6 ("wino"), 64 tiles (256 pixels) x 64 channels
-        *bm = 256;
-        *bn = 64;
+    if (wino_ok(a, vec_epilogue(a))) {  // reported as mode 6 ("wino"): 64 tiles (256 pixels) x 64 channels,
+        const int wc = wino_item_channels(a);      // or 32 tiles (128 pixels) x 128 channels
+        *bm = wc == 64 ? 256 : 128;
+        *bn = wc;
         *mode = 6;
         if (ksplit) {
             const size_t need = wino_workspace_bytes(a);

@@ -50,6 +50,7 @@ namespace pu {
 
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int WG_BM = 64;                      // tiles per block
 constexpr int WG_BN = 64;                      // output channels per block
@@ -529,6 +530,387 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------------ 128-channel Winograd items
+// wino128_x6_kernel: the same F(2x2,3x3) arithmetic, products and output transform as
+// wino_x6_kernel, with items of 32 tiles x 128 output channels instead of 64 x 64, so each V
+// element formed feeds 128 outputs instead of 64 (half the formation work per MFMA; a layer's V is
+// formed once per 128 channels) at the price of twice the U bytes per MFMA (a 48 KB U slice per
+// sub-stage).  8 waves (wn, wx): 32 tiles x 32 channels (32 wn ..) x the 8 positions of j = 2wx,
+// 2wx+1 - 128 accumulators, as in wino_x6_kernel.  Thread (tile tt, channel q) holds the 4x4
+// window of one channel and forms its V row per sub-stage (4 values, exact 3-term split, 12
+// 2-byte plane stores).  LDS: V 2 x 12 KB, U 2 x 48 KB (U issued one sub-stage ahead; the slice is
+// L2-resident - every item of an XCD shares it, channel block slowest), 120 KB.
+#ifndef PU_W2_ABL
+#define PU_W2_ABL 0     // wino128_x6_kernel ablations (timing only, wrong results): 1 no U DMA, 2 no V formation
+#endif
+constexpr int W2_BM = 32;
+constexpr int W2_BN = 128;
+constexpr int W2_VH = 4 * 3 * W2_BM * 32;      // 12 KB
+constexpr int W2_UH = 4 * 3 * W2_BN * 32;      // 48 KB
+
+__device__ __forceinline__ void split3_quad(const f32x4 x, bf16x4_t& h, bf16x4_t& m, bf16x4_t& l) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const __bf16 a = (__bf16)x[e];
+        const float r = x[e] - (float)a;
+        const __bf16 b = (__bf16)r;
+        h[e] = a;
+        m[e] = b;
+        l[e] = (__bf16)(r - (float)b);
+    }
+}
+
+template <bool PERSIST>
+__global__ __launch_bounds__(512) void wino128_x6_kernel(const WinoParams w) {
+#pragma clang fp contract(off)
+    const IgemmParams& p = w.p;
+    __shared__ __attribute__((aligned(16))) unsigned char ldv0[W2_VH];
+    __shared__ __attribute__((aligned(16))) unsigned char ldv1[W2_VH];
+    __shared__ __attribute__((aligned(16))) unsigned char ldu0[W2_UH];
+    __shared__ __attribute__((aligned(16))) unsigned char ldu1[W2_UH];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wn = wave & 3, wx = wave >> 2;
+    const int per_split = w.gm * p.gn;
+    const int total = per_split * p.ksplit;
+
+    int it, end, step;
+    if (PERSIST) {
+        const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+        const int q8 = total >> 3, r8 = total & 7;
+        const int start = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+        end = start + q8 + (xcd < r8 ? 1 : 0);
+        it = start + local;
+        step = (int)(gridDim.x >> 3);
+    } else {
+        it = xcd_remap(blockIdx.x, gridDim.x);
+        end = it + 1;
+        step = 1;
+    }
+    if (it >= end) return;
+
+    // ---- producer role: tile tt of the item, channel q of each 16-channel chunk
+    const int tt = tid >> 4, q = tid & 15;
+    const int cs = p.c0;
+    const int shift = p.Wi + 1;
+    const unsigned pixb = (unsigned)cs * 4u;
+    const float* a0 = p.src0 - (long long)shift * cs;
+    const float* a1 = (p.c1 ? p.src1 : p.src0) - (long long)shift * cs;
+    const int v_st = tt * 32 + (((q >> 3) ^ ((tt >> 3) & 1)) * 16) + (q & 7) * 2;
+
+    // ---- U loader: wave w fills pieces 6w .. 6w+5 (piece P = (j*3 + plane)*4 + row quarter)
+    const unsigned u_lane = (unsigned)((lane >> 1) * 32 + (((lane & 1) ^ ((lane >> 4) & 1)) * 16));
+    const unsigned u_row = (unsigned)p.N * 32u;
+    unsigned poff[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        const int P = wave * 6 + e;
+        poff[e] = (unsigned)(P >> 2) * u_row + (unsigned)((P & 3) * 1024);
+    }
+
+    // ---- MFMA role: positions j = 2wx, 2wx+1; U rows 32*wn + (lane&31), V rows lane&31
+    const int rd_sw = (((lane >> 5) ^ ((lane >> 3) & 1)) * 16);
+    const int u_rd = (32 * wn + (lane & 31)) * 32 + rd_sw + 2 * wx * 3 * 4096;
+    const int v_rd = (lane & 31) * 32 + rd_sw + 2 * wx * 3 * 1024;
+
+    struct Item {
+        int kz, m_blk, n_blk, kc0, kc1;
+        unsigned vrow[4];
+        bool c0ok, c3ok, live;
+    };
+    auto decode = [&](int item, Item& I) {
+        I.live = item < end;
+        I.kz = item / per_split;
+        const int rest = item - I.kz * per_split;
+        const int nb = rest / w.gm;
+        I.m_blk = (rest - nb * w.gm) * W2_BM;
+        I.n_blk = nb * W2_BN;
+        I.kc0 = I.kz * w.kc_per;
+        I.kc1 = min(p.C / 16, I.kc0 + w.kc_per);
+        const int m = I.m_blk + tt;
+        int ty = 0, tx = 0, b = 0;
+        const bool mv = I.live && m < w.tiles;
+        if (mv) {
+            const int t2 = fdiv(m, w.dTw);
+            tx = m - t2 * (p.Wo >> 1);
+            b = fdiv(t2, w.dTh);
+            ty = t2 - b * (p.Ho >> 1);
+        }
+        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + q * 4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            I.vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
+        I.c0ok = x0 >= 0;
+        I.c3ok = x0 + 3 < p.Wi;
+    };
+    Item cur, nxt;
+    decode(it, cur);
+    decode(it + step, nxt);
+
+    float d[16];
+    f32x16 acc[8];
+
+    auto load_row = [&](const Item& I, int kc, int rr) {
+        const int c = kc * 16;
+        const bool second = c >= p.c0;
+        const bool ok = I.live && kc < I.kc1;
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, ok ? w.a_bytes : 0u);
+        const unsigned cb = (unsigned)((second ? c - p.c0 : c) * 4);
+#pragma unroll
+        for (int ss = 0; ss < 4; ++ss) {
+            unsigned vo = I.vrow[rr];
+            if (ss == 0) vo = I.c0ok ? vo : LEAN_OOB;
+            if (ss == 3) vo = I.c3ok ? vo : LEAN_OOB;
+            const unsigned soff = __builtin_amdgcn_readfirstlane(cb + ss * pixb);
+            d[rr * 4 + ss] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, soff, 0));
+        }
+    };
+    auto load_u = [&](const Item& I, int kc, int i, unsigned char* base) {
+        if (PU_W2_ABL == 1) return;
+        const unsigned bytes = I.live && kc < I.kc1 ? w.u_bytes : 0u;
+        const unsigned sb = (unsigned)((kc * 16 + 4 * i) * 3) * u_row + (unsigned)(I.n_blk * 32);
+#pragma unroll
+        for (int e = 0; e < 6; ++e) lean_load(w.U, bytes, base + (wave * 6 + e) * 1024, u_lane, sb + poff[e]);
+    };
+    // V = row i of B^T d B for this thread's channel -> hi/mid/lo planes in V slot sb
+    auto make_v = [&](auto i_c, unsigned char* sb) {
+        constexpr int i = decltype(i_c)::value;
+        if (PU_W2_ABL == 2) return;
+        float t[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            if constexpr (i == 0) t[s2] = d[s2] - d[8 + s2];
+            else if constexpr (i == 1) t[s2] = d[4 + s2] + d[8 + s2];
+            else if constexpr (i == 2) t[s2] = d[8 + s2] - d[4 + s2];
+            else t[s2] = d[4 + s2] - d[12 + s2];
+        }
+        const f32x4 v = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+        bf16x4_t h, m, l;
+        split3_quad(v, h, m, l);
+        unsigned char* base = sb + v_st;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            *reinterpret_cast<__bf16*>(base + (j * 3 + 0) * 1024) = h[j];
+            *reinterpret_cast<__bf16*>(base + (j * 3 + 1) * 1024) = m[j];
+            *reinterpret_cast<__bf16*>(base + (j * 3 + 2) * 1024) = l[j];
+        }
+    };
+    auto mma = [&](auto x_c, const unsigned char* sv, const unsigned char* su, int jj) {
+        constexpr int x = decltype(x_c)::value;
+        const unsigned char* ub = su + u_rd + jj * 3 * 4096;
+        const unsigned char* vb = sv + v_rd + jj * 3 * 1024;
+        bf16x8_t fu[3], fv[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            fu[pl] = *reinterpret_cast<const bf16x8_t*>(ub + pl * 4096);
+            fv[pl] = *reinterpret_cast<const bf16x8_t*>(vb + pl * 1024);
+        }
+        f32x16 c = acc[x];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[1], fv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[2], fv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[0], fv[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[1], fv[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[0], fv[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fu[0], fv[0], c, 0, 0, 0);
+        acc[x] = c;
+    };
+    using I0 = std::integral_constant<int, 0>;
+
+    // sub-stage (kc, i): V slot i & 1 (formed during the previous sub-stage), U slot i & 1 (issued
+    // during the previous sub-stage).  Issues U of the stream's next sub-stage into the other slot
+    // (read by the previous sub-stage, which every wave has left at the barrier) and the window
+    // rows of the next chunk that this chunk no longer reads (row 0 in i = 0, row 2 in i = 1, rows
+    // 1 and 3 in i = 2).  Wait counts: the rows issued after U in the previous sub-stage.
+    auto sub = [&](int kc, const Item& T, int tkc, auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        unsigned char* cv = (i & 1) ? ldv1 : ldv0;
+        unsigned char* nv = (i & 1) ? ldv0 : ldv1;
+        unsigned char* cu = (i & 1) ? ldu1 : ldu0;
+        unsigned char* fu = (i & 1) ? ldu0 : ldu1;
+        if constexpr (i == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else if constexpr (i == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else if constexpr (i == 2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if constexpr (i < 3) load_u(cur, kc, i + 1, fu);
+        else load_u(T, tkc, 0, fu);
+        asm volatile("" ::: "memory");                  // the wait counts assume U is issued first
+        if constexpr (i == 0) load_row(T, tkc, 0);
+        mma(std::integral_constant<int, 2 * i>{}, cv, cu, 0);
+        if constexpr (i < 3) make_v(std::integral_constant<int, i + 1>{}, nv);
+        else make_v(I0{}, nv);
+        if constexpr (i == 1) load_row(T, tkc, 2);
+        if constexpr (i == 2) {
+            load_row(T, tkc, 1);
+            load_row(T, tkc, 3);
+        }
+        mma(std::integral_constant<int, 2 * i + 1>{}, cv, cu, 1);
+    };
+
+    // stream prologue: the first item's whole first window and U of its sub-stage 0, V of 0
+    load_row(cur, cur.kc0, 0);
+    load_row(cur, cur.kc0, 1);
+    load_row(cur, cur.kc0, 2);
+    load_row(cur, cur.kc0, 3);
+    load_u(cur, cur.kc0, 0, ldu0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    make_v(I0{}, ldv0);
+
+    // output-transform exchange through U slot 1 (free at an item boundary: the last sub-stage
+    // read it; the next item's U(0) is in slot 0): [wn][wx][2][4][64] floats = 16 KB per round
+    float* xs = reinterpret_cast<float*>(ldu1) + (wn * 2 + wx) * 512;
+    const float* xr = reinterpret_cast<const float*>(ldu1) + (wn * 2 + (1 - wx)) * 512;
+
+    while (true) {
+#pragma unroll
+        for (int x = 0; x < 8; ++x)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+        for (int kc = cur.kc0; kc < cur.kc1; ++kc) {
+            const bool last = kc + 1 >= cur.kc1;
+            const Item& T = last ? nxt : cur;
+            const int tkc = last ? nxt.kc0 : kc + 1;
+            sub(kc, T, tkc, std::integral_constant<int, 0>{});
+            sub(kc, T, tkc, std::integral_constant<int, 1>{});
+            sub(kc, T, tkc, std::integral_constant<int, 2>{});
+            sub(kc, T, tkc, std::integral_constant<int, 3>{});
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+
+        // output transform, as wino_x6_kernel (wave wx finishes output row py = wx of the tile)
+        float y0v[16], y1v[16];
+#pragma unroll
+        for (int rd = 0; rd < 4; ++rd) {
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int r = rd * 4 + r4;
+                float sp[2][2];
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    sp[0][jj] = acc[0 * 2 + jj][r] + acc[1 * 2 + jj][r] + acc[2 * 2 + jj][r];
+                    sp[1][jj] = acc[1 * 2 + jj][r] - acc[2 * 2 + jj][r] - acc[3 * 2 + jj][r];
+                }
+                if (wx == 0) {
+                    y0v[r] = sp[0][0] + sp[0][1];
+                    y1v[r] = sp[0][1];
+                    xs[r4 * 64 + lane] = sp[1][0] + sp[1][1];
+                    xs[(4 + r4) * 64 + lane] = sp[1][1];
+                } else {
+                    y0v[r] = sp[1][0];
+                    y1v[r] = sp[1][0] + sp[1][1];
+                    xs[r4 * 64 + lane] = sp[0][0];
+                    xs[(4 + r4) * 64 + lane] = sp[0][0] + sp[0][1];
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int r = rd * 4 + r4;
+                const float o0 = xr[r4 * 64 + lane], o1 = xr[(4 + r4) * 64 + lane];
+                if (wx == 0) {
+                    y0v[r] = y0v[r] + o0;
+                    y1v[r] = y1v[r] - o1;
+                } else {
+                    y0v[r] = o0 + y0v[r];
+                    y1v[r] = o1 - y1v[r];
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        const int e_m = cur.m_blk + (lane & 31), e_n = cur.n_blk + 32 * wn + 4 * (lane >> 5);
+        const bool e_ok = e_m < w.tiles;
+        const int em = e_ok ? e_m : 0;
+        const int t2 = fdiv(em, w.dTw);
+        const int tx = em - t2 * (p.Wo >> 1);
+        const int b = fdiv(t2, w.dTh);
+        const int ty = t2 - b * (p.Ho >> 1);
+        const long long pix0 = ((long long)b * p.Ho + 2 * ty + wx) * p.Wo + 2 * tx;
+        if (p.ksplit == 1) {
+            // the batched float4 epilogue of wino_x6_kernel; a wave's 32 channels lie in one
+            // destination (n0 % 32 == 0, host)
+            const bool first = cur.n_blk + 32 * wn < p.n0;
+            const int ld = first ? p.n0 : p.N - p.n0;
+            float* dst = first ? p.dst0 : p.dst1;
+            const float* msk = first ? p.mask0 : p.mask1;
+            const bool relu = p.flags & PU_EPI_RELU, accum = p.flags & PU_EPI_ACCUM;
+            constexpr unsigned FULL = 0x7fffffffu;
+            const __amdgpu_buffer_rsrc_t r_dst = uniform_rsrc(dst, FULL);
+            const __amdgpu_buffer_rsrc_t r_acc = uniform_rsrc(dst, accum ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_res = uniform_rsrc(p.resid, p.resid ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_msk = uniform_rsrc(msk, msk ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_bias = uniform_rsrc(p.bias, p.bias ? FULL : 0u);
+            const __amdgpu_buffer_rsrc_t r_cs = uniform_rsrc(p.cscale, p.cscale ? FULL : 0u);
+            const unsigned o_px = e_ok ? (unsigned)(pix0 * ld + e_n - (first ? 0 : p.n0)) * 4u : LEAN_OOB;
+            const unsigned o_row = (unsigned)ld * 4u;
+            const unsigned o_cs = (unsigned)(b * p.cs_ld + e_n) * 4u;
+            f32x4 bv[4], sv[4], rv[4][2], mv[4][2], av[4][2];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                bv[g] = epi_ld4(r_bias, (unsigned)(e_n + 8 * g) * 4u);
+                sv[g] = epi_ld4(r_cs, o_cs + 32u * g);
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    const unsigned off = o_px + o * o_row + 32u * g;
+                    rv[g][o] = epi_ld4(r_res, off);
+                    mv[g][o] = epi_ld4(r_msk, off);
+                    av[g][o] = epi_ld4(r_acc, off);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                asm volatile("" :: "v"(bv[g]), "v"(sv[g]));
+#pragma unroll
+                for (int o = 0; o < 2; ++o) asm volatile("" :: "v"(rv[g][o]), "v"(mv[g][o]), "v"(av[g][o]));
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 y[2] = {{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]},
+                                    {y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]}};
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    f32x4 v = y[o];
+                    if (p.bias) v += bv[g];
+                    if (p.resid) v += rv[g][o];
+                    if (relu) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                    }
+                    if (msk) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) if (!(mv[g][o][e] > 0.f)) v[e] = 0.f;
+                    }
+                    if (p.cscale) v *= sv[g];
+                    if (accum) v += av[g][o];
+                    epi_st4(r_dst, o_px + o * o_row + 32u * g, v);
+                }
+            }
+        } else if (e_ok) {
+            float* part = p.part + (long long)cur.kz * p.M * p.N + pix0 * p.N + e_n;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                *reinterpret_cast<f32x4*>(part + 8 * g) = f32x4{y0v[4 * g], y0v[4 * g + 1], y0v[4 * g + 2], y0v[4 * g + 3]};
+                *reinterpret_cast<f32x4*>(part + p.N + 8 * g) = f32x4{y1v[4 * g], y1v[4 * g + 1], y1v[4 * g + 2], y1v[4 * g + 3]};
+            }
+        }
+        if (!nxt.live) break;
+        it += step;
+        cur = nxt;
+        decode(it + step, nxt);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // U = G g G^T per (n, 8 consecutive c), fp64 then rounded to fp32 and split into hi/mid/lo bf16:
 // out[((c/16*16 + xi)*3 + plane)*N + n][c % 16].  Forward: g = w[n][c]; dgrad (the transposed,
 // flipped kernel of the data gradient): output channel n = input channel of w, c = its output
@@ -627,6 +1009,20 @@ __global__ __launch_bounds__(256) void wino_pack_kernel(const WinoPackBatch bt) 
 // 16-channel chunks from one source each with one pixel stride (c1 == 0 or c1 == c0), an even
 // number of chunks, 64-channel output blocks, the float4 epilogue, no ConvT shuffle, buffers
 // addressable with 32-bit offsets
+// 128-channel items (wino128_x6_kernel) for layers with n % 128 == 0: opt-in, PU_WINO128=1 - they
+// measured slower than the 64 x 64 items on every C2 layer (profiles/r05_experiments/wino128_ab.txt)
+static bool wino128_on() {
+    static const bool on = [] {
+        const char* e = getenv("PU_WINO128");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+static bool wino128_use(const pu_conv_args* a) {
+    return wino128_on() && a->n % W2_BN == 0 && (a->n0 == a->n || a->n0 % 32 == 0);
+}
+
 bool wino_ok(const pu_conv_args* a, bool vec_epi) {
     const int C = a->c0 + a->c1;
     if (!a->wino || !a->weight6) return false;
@@ -637,14 +1033,14 @@ bool wino_ok(const pu_conv_args* a, bool vec_epi) {
     // a short reduction (4 chunks) over several 64-channel output blocks re-forms the same V once
     // per block for little MFMA work: the concat layers' data gradients (64 -> 128 / 256) stay
     // on the direct kernel (measured: top_cat dgrad 0.43 vs 0.41 ms, l2_cat 0.21 vs 0.20)
-    if (C < 128 && a->n > WG_BN) return false;
+    if (C < 128 && a->n > WG_BN && !wino128_use(a)) return false;
     const long long px = (long long)a->batch * a->in_h * a->in_w + a->in_w + 1;
     if (px * a->c0 * 4 >= (1LL << 31)) return false;
     if ((long long)C * a->n * 96 >= (1LL << 31)) return false;
     // the epilogue's 32-bit destination offsets and item-uniform destination (64-channel items
     // never straddle the split column n0)
     if ((long long)a->batch * a->out_h * a->out_w * a->n * 4 >= (1LL << 31) - 64) return false;
-    if (a->n0 != a->n && a->n0 % WG_BN) return false;
+    if (a->n0 != a->n && a->n0 % (wino128_use(a) ? 32 : WG_BN)) return false;
     return ((uintptr_t)a->wino & 15) == 0;
 }
 
@@ -653,7 +1049,8 @@ bool wino_ok(const pu_conv_args* a, bool vec_epi) {
 void wino_plan(const pu_conv_args* a, int* ksplit, int* kc_per) {
     const int C = a->c0 + a->c1;
     const long long tiles = (long long)a->batch * (a->out_h / 2) * (a->out_w / 2);
-    const int blocks = ceil_div(tiles, WG_BM) * (a->n / WG_BN);
+    const bool w128 = wino128_use(a);
+    const int blocks = ceil_div(tiles, w128 ? W2_BM : WG_BM) * (a->n / (w128 ? W2_BN : WG_BN));
     const int chunks = C / 16;
     *ksplit = 1;
     *kc_per = chunks;
@@ -681,8 +1078,9 @@ int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     w.p = p;
     w.U = reinterpret_cast<const __bf16*>(a->wino);
     w.tiles = a->batch * (a->out_h / 2) * (a->out_w / 2);
-    w.gm = ceil_div(w.tiles, WG_BM);
-    w.p.gn = a->n / WG_BN;
+    const bool w128 = wino128_use(a);
+    w.gm = ceil_div(w.tiles, w128 ? W2_BM : WG_BM);
+    w.p.gn = a->n / (w128 ? W2_BN : WG_BN);
     w.dTw = make_fastdiv(a->out_w / 2);
     w.dTh = make_fastdiv(a->out_h / 2);
     w.a_bytes = (unsigned)(((long long)a->batch * a->in_h * a->in_w + a->in_w + 1) * a->c0 * 4);
@@ -697,12 +1095,21 @@ int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     w.p.part = (float*)a->workspace;
     w.kc_per = per;
     const int items = w.gm * w.p.gn * ks;
+    if (w128) {
+        if (wino_persist() && items > 256)
+            hipLaunchKernelGGL(wino128_x6_kernel<true>, dim3(256), dim3(512), 0, s, w);
+        else
+            hipLaunchKernelGGL(wino128_x6_kernel<false>, dim3((unsigned)items), dim3(512), 0, s, w);
+        return ks;
+    }
     if (wino_persist() && items > 256)
         hipLaunchKernelGGL(wino_x6_kernel<true>, dim3(256), dim3(512), 0, s, w);
     else
         hipLaunchKernelGGL(wino_x6_kernel<false>, dim3((unsigned)items), dim3(512), 0, s, w);
     return ks;
 }
+
+int wino_item_channels(const pu_conv_args* a) { return wino128_use(a) ? W2_BN : WG_BN; }
 
 size_t wino_workspace_bytes(const pu_conv_args* a) {
     int ks, per;

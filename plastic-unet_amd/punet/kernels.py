@@ -83,6 +83,10 @@ def set_wino(on):
     return prev
 
 
+# the library's PU_WINO128 switch (csrc/winograd.hip reads the same variable once per process)
+_WINO128 = os.environ.get("PU_WINO128", "0") == "1"
+
+
 def wino_wanted(w, mode):
     """Whether a packed conv operand of parameter w (OIHW 3x3) should carry a Winograd operand:
     the reduced channel count a multiple of 32 and the produced one of 64 (the kernel's chunks
@@ -90,7 +94,8 @@ def wino_wanted(w, mode):
     if mode not in (0, 1) or w.dim() != 4 or w.shape[2:] != (3, 3) or _FP32_MATH != "split6":
         return False
     n, c = (w.shape[0], w.shape[1]) if mode == 0 else (w.shape[1], w.shape[0])
-    return c % 32 == 0 and n % 64 == 0 and (c >= 128 or n <= 64)   # csrc wino_ok
+    # csrc wino_ok: a 64-channel reduction into more than 64 outputs only on 128-channel items
+    return c % 32 == 0 and n % 64 == 0 and (c >= 128 or n <= 64 or (_WINO128 and n % 128 == 0))
 
 
 def pack_wino(jobs):

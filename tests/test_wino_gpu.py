@@ -53,6 +53,11 @@ CASES = [
     # epilogue, per-XCD item ranges)
     (5, 128, 128, 64, 0, 64),     # 320 items, 40 per XCD
     (3, 96, 80, 128, 0, 192),     # 270 items: ragged per-XCD ranges (270 % 8 = 6), 3 channel blocks
+    # n % 128 == 0 shapes (the 128-channel items under PU_WINO128=1 - test_wino128_bit_identical_..)
+    (2, 16, 16, 128, 0, 256),     # 2 channel blocks of 128
+    (5, 128, 128, 64, 0, 128),    # 64 -> 128 (direct before 128-channel items), 640 items, persistent
+    (7, 96, 80, 128, 0, 128),     # 420 items: ragged per-XCD ranges (420 % 8 = 4)
+    (2, 24, 24, 64, 64, 64),      # its data gradient: 64 -> 128 split at 64 (the top concat layer)
 ]
 
 
@@ -76,7 +81,8 @@ def test_wino_fwd_dgrad_vs_fp64(B, H, W, c0, c1, cout):
         xk = nhwc(x).to(DEV)
         x0, x1 = (xk[..., :c0].contiguous(), xk[..., c0:].contiguous()) if c1 else (xk, None)
         wk = w.to(DEV)
-        assert getattr(pk.get(wk, 0, K.round16(9 * C), K.cgroup_for(c0, c1)), "_wino", None) is not None
+        assert (getattr(pk.get(wk, 0, K.round16(9 * C), K.cgroup_for(c0, c1)), "_wino", None) is not None) \
+            == K.wino_wanted(wk, 0)
         y = T.conv3x3(x0, wk, b.to(DEV), pk, x1=x1, relu=True)
         check("wino fwd %dx%dx%d %d+%d->%d" % (B, H, W, c0, c1, cout), nchw(y), ref[torch.float32][0],
               ref[torch.float64][0])
@@ -214,3 +220,50 @@ def test_wino_wgrad_vs_fp64(B, H, W, c0, c1, cout):
     check("wino bias grad", db, ref[torch.float32][1], ref[torch.float64][1])
     dw2, db2 = T.conv3x3_wgrad(dzk, x0, x1)
     assert torch.equal(dw, dw2) and torch.equal(db, db2), "Winograd weight gradient is not deterministic"
+
+
+_W128_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from punet import kernels as K, trunk as T
+out = {}
+for (B, H, W, c0, c1, N) in [(3, 32, 24, 128, 0, 128), (2, 16, 16, 256, 0, 256), (2, 32, 32, 128, 128, 128),
+                             (4, 8, 8, 512, 0, 512), (9, 64, 64, 128, 0, 128)]:
+    g = torch.Generator().manual_seed(B + H + c0 + c1 + N)
+    C = c0 + c1
+    x = torch.randn(B, H, W, C, generator=g).relu().cuda()
+    w = (torch.randn(N, C, 3, 3, generator=g) * 0.05).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    dz = torch.randn(B, H, W, N, generator=g).cuda()
+    pk = T._Packs()
+    x0, x1 = (x[..., :c0].contiguous(), x[..., c0:].contiguous()) if c1 else (x, None)
+    y = T.conv3x3(x0, w, b, pk, x1=x1, relu=True)
+    d0, d1 = T.conv3x3_dgrad(dz, w, pk, split=c0 if c1 else None, mask0=x0, mask1=x1)
+    out[(B, H, W, c0, c1, N)] = (y.cpu(), d0.cpu(), None if d1 is None else d1.cpu())
+torch.save(out, sys.argv[1])
+"""
+
+
+def test_wino128_bit_identical_to_64_channel_items(tmp_path):
+    """32-tile x 128-channel Winograd items (wino128_x6_kernel) and 64 x 64 items (PU_WINO128=0,
+    read once per process - two child processes) feed every accumulator the same U / V fragments
+    in the same MFMA order, then the same output transform: forward and data gradient bitwise equal
+    on the layers both take (n % 128 == 0, C >= 128; split-K, concat sources, split outputs,
+    persistent item streams)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plastic-unet_amd")
+    res = {}
+    for on in ("1", "0"):
+        f = str(tmp_path / ("w%s.pt" % on))
+        env = dict(os.environ, PU_WINO128=on, PU_WINO="1")
+        r = subprocess.run([sys.executable, "-c", _W128_SCRIPT, f, root], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[on] = torch.load(f, weights_only=True)
+    for k in res["1"]:
+        for a, b in zip(res["1"][k], res["0"][k]):
+            assert (a is None) == (b is None), k
+            if a is not None:
+                assert torch.equal(a, b), k
