@@ -944,18 +944,37 @@ __global__ __launch_bounds__(256) void wino_pack_kernel(const WinoPackBatch bt) 
     const int n0 = (blk % nblks) * WP_N, c0 = (blk / nblks) * WP_C;
     const int nn = min(WP_N, J.n - n0), cc = min(WP_C, J.c - c0);
     const int tid = threadIdx.x;
-    // stage g[n][c][3][3] (dgrad: g[r][s] = w[c][n][2-r][2-s], flipped when read below)
-    if (!J.dgrad) {
-        for (int e = tid; e < WP_N * WP_C * 9; e += 256) {
-            const int nl = e / (WP_C * 9), rest = e - nl * WP_C * 9;
-            if (nl < nn && rest < cc * 9) gw[nl * WP_LD + rest] = J.w[((long long)(n0 + nl) * J.c + c0) * 9 + rest];
+    // stage g[n][c][3][3] (dgrad: g[r][s] = w[c][n][2-r][2-s], flipped when read below).  A thread
+    // stages 72 floats in 3 groups of 24 loads issued back to back (out-of-tile lanes load element 0
+    // and drop it), so the tile costs 3 memory round trips rather than one per element.
+    constexpr int PER = WP_N * WP_C * 9 / 256, GRP = 24;
+    static_assert(PER % GRP == 0, "staging groups");
+#pragma unroll
+    for (int g0 = 0; g0 < PER; g0 += GRP) {
+        float v[GRP];
+        int dst[GRP];
+#pragma unroll
+        for (int u = 0; u < GRP; ++u) {
+            const int e = tid + (g0 + u) * 256;
+            long long src;
+            bool ok;
+            if (!J.dgrad) {
+                const int nl = e / (WP_C * 9), rest = e - nl * WP_C * 9;
+                ok = nl < nn && rest < cc * 9;
+                src = ((long long)(n0 + nl) * J.c + c0) * 9 + rest;
+                dst[u] = ok ? nl * WP_LD + rest : -1;
+            } else {
+                const int cl = e / (WP_N * 9), rest = e - cl * WP_N * 9;
+                const int nl = rest / 9, k = rest - nl * 9;
+                ok = cl < cc && nl < nn;
+                src = ((long long)(c0 + cl) * J.n + n0) * 9 + rest;
+                dst[u] = ok ? nl * WP_LD + cl * 9 + k : -1;
+            }
+            v[u] = J.w[ok ? src : 0];
         }
-    } else {
-        for (int e = tid; e < WP_C * WP_N * 9; e += 256) {
-            const int cl = e / (WP_N * 9), rest = e - cl * WP_N * 9;
-            const int nl = rest / 9, k = rest - nl * 9;
-            if (cl < cc && nl < nn) gw[nl * WP_LD + cl * 9 + k] = J.w[((long long)(c0 + cl) * J.n + n0) * 9 + rest];
-        }
+#pragma unroll
+        for (int u = 0; u < GRP; ++u)
+            if (dst[u] >= 0) gw[dst[u]] = v[u];
     }
     __syncthreads();
     const int half = tid & 1, nl = (tid >> 1) & 31, ch = tid >> 6;
