@@ -60,6 +60,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-profile", action="store_true")
     ap.add_argument("--no-oja", action="store_true", help="skip the Oja-update HBM benchmark")
+    ap.add_argument("--graph", choices=["on", "off"], default="off",
+                    help="on: fwd + BCE + bwd captured once as a HIP graph and replayed (one rank only). "
+                         "Off by default: measured no faster on C2 / C4 and slower on C3, whose replay loses "
+                         "the weight-gradient side stream's overlap (profiles/r05_experiments/graph_step_ab.txt)")
     a = ap.parse_args()
     dflt = {"c2": (32, 128), "c3": (32, 128), "c4": (32, 256), "c5": (16, 512)}[a.config]
     a.batch = a.batch or dflt[0]
@@ -292,7 +296,7 @@ def main():
     net = build_model(args, device)
     net.train()
     dp.broadcast_params(net)
-    trainer = Trainer(net, lr=args.lr, steplr=args.steplr)
+    trainer = Trainer(net, lr=args.lr, steplr=args.steplr, graph=(world == 1 and args.graph == "on"))
 
     B, S = args.batch, args.img
     g = torch.Generator().manual_seed(1234 + rank)
@@ -358,12 +362,14 @@ def main():
         from punet import trunk as _trunk
         side = _trunk._SIDE
         _trunk.set_side_stream(False)
+        graph, trainer.graph = trainer.graph, False      # eager steps: the profiler wraps each launch
         try:
             with K.KernelProfiler() as prof:
                 for i in range(nprof):
                     loss, hebb = trainer.step(xs[i % NB], ts[i % NB], hebb)
         finally:
             _trunk.set_side_stream(side)
+            trainer.graph = graph
         summ = prof.summary()
         kern = {}
         for tag, d in sorted(summ.items(), key=lambda kv: -kv[1]["ms"]):
@@ -459,6 +465,8 @@ def main():
             "config": {"workload": CONFIGS[args.config] % vars(args),
                        "global_batch": world * B, "per_gpu_batch": B, "img": S,
                        "parallelism": "dp%d" % world if world > 1 else "single",
+                       "step_launch": "hip_graph (fwd + BCE + bwd replayed, Adam eager)" if trainer.graph
+                       else "eager",
                        "fp32_gemm": None if args.config == "c3" else
                        {"split6": "fp32 operands split exactly into 3 bf16 terms, 6 bf16 MFMA products per fp32 "
                                   "product, fp32 accumulation (error of an fp32 product)",

@@ -3,6 +3,13 @@
     trainer = Trainer(net, lr=3e-4, steplr=1e5)     # FusedAdam + StepLR(gamma .666), per step
     loss, hebb = trainer.step(x, t, hebb)           # fwd -> BCE -> bwd (+ overlapped RCCL all-reduce) -> Adam
 
+Trainer(..., graph=True) (one rank): after two eager steps the forward + BCE + backward of a step is
+captured once into a HIP graph and replayed; the inputs are copied into the graph's static tensors
+and the optimizer step runs eagerly after each replay.  The graph holds every kernel launch of the
+step - the trunk's operand packing included (captured right after an optimizer step, when every
+packed operand is stale) - so the host issues one graph launch instead of several hundred kernel
+launches; the kernels and their order are the eager step's (bit-identical results).
+
 Batched semantics: slot b of step s carries its trace to slot b of step
 s+1; loss = mean BCE over all slots' pixels (so each slot contributes the reference's per-sample
 gradient / B).  Under data parallelism each rank runs its own slots (the global batch is sharded
@@ -18,7 +25,7 @@ from .optim import FusedAdam
 
 class Trainer:
     def __init__(self, net, lr=3e-4, steplr=1e5, gamma=0.666, betas=(0.9, 0.999), eps=1e-8,
-                 flat_grads=True, bucket_mb=16, overlap=True, force_reduce=False):
+                 flat_grads=True, bucket_mb=16, overlap=True, force_reduce=False, graph=False):
         """force_reduce: run the overlapped all-reduce path even in a world of one rank (tests the
         RCCL async path on a one-GPU box; an AVG over one rank is the identity)"""
         self.net = net
@@ -41,6 +48,11 @@ class Trainer:
             if self.distributed and overlap:
                 self.reducer = dp.BucketReducer(self.gradbuf, bucket_mb=bucket_mb, force=force_reduce)
         self.overlapped_buckets = 0
+        # HIP-graph step (one rank only: the overlapped all-reduce issues collectives from the host
+        # during backward); eager warm-up steps first, then capture
+        self.graph = bool(graph) and not self.distributed
+        self._graph = None
+        self._graph_warm = 0
         # all-reduce accounting (bench.py's `allreduce` block): set measure_allreduce = True and
         # every step appends (buckets issued, issued during backward, exposed ms) to allreduce_log.
         # Exposed time = the compute stream's wait for the collectives: a HIP event after the last
@@ -89,7 +101,45 @@ class Trainer:
 
     def step(self, x, t, hebb):
         """One optimisation step on the local batch.  Returns (loss tensor, new hebb), both
-        detached and still on the device (no host synchronisation)."""
+        detached and still on the device (no host synchronisation).  With graph=True the returned
+        hebb is the graph's output tensor: the next step overwrites it (pass it back in as usual)."""
+        if self.graph and x.is_cuda:
+            if self._graph is not None or self._graph_warm >= 2:
+                return self._graph_step(x, t, hebb)
+            self._graph_warm += 1
+        return self._eager_step(x, t, hebb)
+
+    def _graph_step(self, x, t, hebb):
+        if self._graph is None:
+            # capture right after an (eager) optimizer step: every packed operand is stale, so the
+            # trunk's refresh launches are part of the graph and run on every replay
+            self._sx = x.detach().clone()
+            self._st = t.detach().clone()
+            self._sh = hebb.detach().clone()
+            for p in self.params:
+                p.grad = None
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                y, hn = self.net(self._sx, self._sh)
+                loss = bce_loss(y, self._st)
+                loss.backward()
+            self._graph = g
+            self._gloss, self._ghn = loss.detach(), hn.detach()
+            self._ggrads = [p.grad for p in self.params]
+        else:
+            self._sx.copy_(x)
+            self._st.copy_(t)
+            if hebb is not self._sh:
+                self._sh.copy_(hebb)
+        self._graph.replay()
+        # the gradients the graph writes (an eager step in between may have rebound .grad)
+        for p, gr in zip(self.params, self._ggrads):
+            p.grad = gr
+        self.opt.step()
+        self.sched.step()
+        return self._gloss.clone(), self._ghn
+
+    def _eager_step(self, x, t, hebb):
         for p in self.params:
             p.grad = None
         y, hn = self.net(x, hebb.detach())

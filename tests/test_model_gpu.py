@@ -388,6 +388,46 @@ def test_c2_side_stream_weight_gradients_bitwise(precision):
     assert torch.equal(res[0][3], res[1][3])
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_step_bitwise_equals_eager(precision):
+    """Trainer(graph=True): two eager steps, then fwd + BCE + bwd captured once as a HIP graph and
+    replayed (inputs copied into its static tensors, Adam eager).  Six steps with changing inputs
+    and the trace carried must match eager steps bit for bit - losses, gradients, parameters and
+    the trace - which also checks that the captured operand packing runs on every replay (stale
+    packed weights after the first replay would change the third loss).  An eager step in between
+    (bench.py's profiling pass) must not disturb the replays that follow."""
+    from punet.engine import Trainer
+    res = []
+    for graph in (False, True):
+        _, net, x, t, H = _c2_pair(8, seed=5)
+        if precision == "bf16":
+            sd = net.state_dict()
+            net = UNetp(1, 1, DEV, rule="oja", nbf=128, depth=5, base_ch=64, precision="bf16")
+            net.load_state_dict(sd)
+        tr = Trainer(net, lr=1e-3, steplr=1e5, graph=graph)
+        hebb = H.to(DEV)
+        losses, grads = [], []
+        for s in range(6):
+            if s == 4:
+                tr.graph = False          # one eager step between replays
+            xs = torch.roll(x, shifts=s, dims=0).to(DEV)
+            loss, hebb = tr.step(xs, t.to(DEV), hebb)
+            tr.graph = graph
+            losses.append(loss.item())
+            grads.append({k: p.grad.detach().clone() for k, p in net.named_parameters() if p.grad is not None})
+        torch.cuda.synchronize()
+        assert (tr._graph is not None) == graph
+        res.append((losses, grads, {k: p.detach().clone() for k, p in net.named_parameters()}, hebb.clone()))
+    assert res[0][0] == res[1][0]
+    for s in range(6):
+        assert res[0][1][s].keys() == res[1][1][s].keys()
+        for k in res[0][1][s]:
+            assert torch.equal(res[0][1][s][k], res[1][1][s][k]), (s, k)
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
+    assert torch.equal(res[0][3], res[1][3])
+
+
 def test_lazy_direct_operands_after_optimizer_steps():
     """After an optimizer step the trunk refreshes only the Winograd operand of a layer that has
     only ever run on the Winograd kernel (trunk._Packs.refresh); a later call that takes the direct
