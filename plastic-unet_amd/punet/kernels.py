@@ -175,7 +175,15 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream():
+    """The current stream's raw handle.  torch.cuda.current_stream() resolves the device through
+    torch.cuda.is_available() and an environment lookup on every call (~2 us of host time, several
+    hundred calls per training step); the raw accessor takes the device index directly."""
+    if _RAW_STREAM is not None:
+        return _RAW_STREAM(torch._C._cuda_getDevice())
     return torch.cuda.current_stream().cuda_stream
 
 

@@ -41,6 +41,23 @@ _STEM_BF16 = os.environ.get("PU_STEM_BF16", "1") != "0"
 _LAZY = os.environ.get("PU_LAZY_DIRECT", "1") != "0"
 
 
+class _OnStream:
+    """torch.cuda.stream(s) without its per-call device resolution (host time on the backward's
+    issue path): make s current, restore the previous stream of s's device on exit."""
+    __slots__ = ("s", "prev")
+
+    def __init__(self, s):
+        self.s = s
+
+    def __enter__(self):
+        self.prev = torch.cuda.current_stream(self.s.device_index)
+        torch.cuda.set_stream(self.s)
+
+    def __exit__(self, *exc):
+        torch.cuda.set_stream(self.prev)
+        return False
+
+
 def set_side_stream(on):
     """Switch the weight-gradient side stream for backward passes started after this call:
     True / False, or "bf16" (the default: bf16 trunks only)."""
@@ -324,8 +341,8 @@ class UNetpTrunk:
         if ws is None:
             gb.ready(*self.params[i:i + n])
             return
-        ws.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(ws):
+        ws.wait_stream(torch.cuda.current_stream(ws.device_index))
+        with _OnStream(ws):
             gb.ready(*self.params[i:i + n])
 
     def _wgrad(self, fn, i, out, *reads):
@@ -341,8 +358,8 @@ class UNetpTrunk:
             if out is None:
                 out = (torch.empty_like(self.params[i], memory_format=torch.contiguous_format),
                        torch.empty_like(self.params[i + 1]))
-            ws.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(ws):
+            ws.wait_stream(torch.cuda.current_stream(ws.device_index))
+            with _OnStream(ws):
                 r = fn(out)
             for t in reads:
                 if t is not None:
@@ -451,7 +468,7 @@ class UNetpTrunk:
             return self._backward(s, dlogits, params)
         finally:
             if self._side is not None:
-                torch.cuda.current_stream().wait_stream(self._side)   # grads complete before use
+                torch.cuda.current_stream(self._side.device_index).wait_stream(self._side)   # grads complete before use
                 self._side = None
 
     def _backward(self, s, dlogits, params):
