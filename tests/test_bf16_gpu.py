@@ -213,12 +213,13 @@ def test_bf16_halo_conv_bit_identical_to_lean(c0, cout):
 
 
 @pytest.mark.parametrize("B,H,epi", [(8, 128, "relu"), (8, 128, "mask"), (8, 128, "resid"), (9, 128, "accum"),
-                                     (8, 128, "plain")])
+                                     (8, 128, "plain"), (2, 128, "relu"), (2, 128, "mask")])
 def test_bf16_rows_conv_bit_identical_to_lean(B, H, epi):
     """the row-stream kernel (128-wide 64 -> 64 3x3: weights resident in LDS, 16-row strips) sums
     the same bf16 products in the same order as the per-tap lean kernel: bit-identical outputs with
     every epilogue option (bias + ReLU, mask, residual, accumulate).  B >= 8 keeps the lean kernel
-    unsplit (>= 512 tiles; a K split adds its partial sums in another order)"""
+    unsplit (>= 512 tiles).  At B = 2 the lean plan splits K and adds its fp32 partial sums in
+    another order, so the two bf16 outputs agree to within one bf16 rounding (2 ulp bound)."""
     from punet._lib import PU_PACK_CONV_FWD
     g = torch.Generator(device=DEV).manual_seed(H + B + len(epi))
     x = torch.randn(B, H, 128, 64, device=DEV, generator=g).to(BF)
@@ -241,7 +242,11 @@ def test_bf16_rows_conv_bit_identical_to_lean(B, H, epi):
     finally:
         K.set_conv_halo(prev)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    if B >= 8:
+        assert torch.equal(outs[0], outs[1])
+    else:
+        assert torch.allclose(outs[0].float(), outs[1].float(), rtol=2 ** -7, atol=2 ** -12)
+        assert (outs[0] != outs[1]).float().mean().item() < 0.05
     ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.to(BF).float(), None if epi == "plain" else b,
                                      padding=1).permute(0, 2, 3, 1)
     if epi == "relu":

@@ -13,8 +13,8 @@ and the thresholded masks agree bit for bit away from the threshold.
 Bars (fp32 configs C4/C5): logits / Y / H' within 1e-4 relative of fp64 (north star), per-tensor
 gradient relative L2 2e-3 (ReLU flips at fp32-noise pre-activations).  bf16 (C3):
 the measured error of a bf16 trunk against fp64 with margin - Y within 5e-5, H' within 5e-6, loss
-within 1e-6, gradient relative L2 per tensor < 0.3 and overall < 0.02 (every bf16 kernel alone
-sits at its rounding bound, tests/test_bf16_gpu.py)."""
+within 1e-6, gradient relative L2 per tensor < 0.2 and overall < 0.01 (measured 0.122 / 0.003; every
+bf16 kernel alone sits at its rounding bound, tests/test_bf16_gpu.py)."""
 import pytest
 import torch
 
@@ -116,8 +116,8 @@ def test_c3_bf16_base64_vs_fp64_oracle():
     # 0.003, worst single tensor 0.12 (a bias whose gradient is a sum of bf16-rounded dZ)
     assert ey < 5e-5 and eh < 5e-6
     assert abs(loss.item() - lr_) < 1e-6
-    assert max(rels.values()) < 0.3, rels
-    assert tot < 0.02
+    assert max(rels.values()) < 0.2, rels
+    assert tot < 0.01
 
 
 def test_c3_bf16_bs32_deterministic_and_slot_consistent():
