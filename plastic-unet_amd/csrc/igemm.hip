@@ -186,7 +186,8 @@ __device__ __forceinline__ void epilogue_batched_shuf(const IgemmParams& p, f32x
     for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            bv[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)cj[j] * 4u, 32 * q, 0));
+            bv[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rb, nc0 + j * 32 < p.N ? (unsigned)cj[j] * 4u : LEAN_OOB, 32 * q, 0));
     const __amdgpu_buffer_rsrc_t rd = epi_rsrc(p.dst0, true);
 #pragma unroll
     for (int j = 0; j < FN; ++j)

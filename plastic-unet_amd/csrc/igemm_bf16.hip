@@ -239,7 +239,8 @@ __device__ __forceinline__ void epilogue_batched_shuf_b(const IgemmBf16Params& p
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            bv[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (unsigned)cj[j] * 4u, 32 * q, 0));
+            bv[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rb, nc0 + j * 32 < p.N ? (unsigned)cj[j] * 4u : LEAN_OOB, 32 * q, 0));
     const __amdgpu_buffer_rsrc_t rd = epi_rsrc_b(p.dst0, true);
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
@@ -1465,7 +1466,8 @@ static void plan_lean_b(const pu_conv_args* a, long long M, int* bm, int* bn, in
     // small pixel grids (the 8^2 / 16^2 levels): 128 x 128 tiles split to ~2 blocks per CU.  The
     // 256 x 128 tiles split 8 / 16 ways wrote 8 - 16 fp32 partial tiles per output (67 MB per 8^2
     // layer, read back by the split epilogue) for blocks that ran 1 - 2 channel groups each
-    if (smallm_on() && a->n > 64) {
+    // (PU_BF16_LEAN128=0 with t128 >= 240 keeps the old 256 x 128 split: the A/B switch above)
+    if (smallm_on() && a->n > 64 && (lean128_on() || t128 < 240)) {
         int k2 = ceil_div(target, t128);
         if (k2 > T / 9) k2 = T / 9;
         *bm = 128;

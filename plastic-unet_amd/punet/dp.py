@@ -49,6 +49,23 @@ def broadcast_params(module, src=0):
         torch.autograd.graph.increment_version(ts)
 
 
+def rank_generator(device, seed=None, rank=None):
+    """A per-rank random generator on ``device`` for the trunk's Dropout2d masks
+    (unet_p_res.py:62,69).  Parameters start identical on every rank (broadcast_params), but the
+    masks must not: with one shared seed every rank would draw the same channel mask for its slot
+    b, so a world of R ranks x B slots would see only B distinct mask sets instead of R x B (the
+    single-process global batch).  seed defaults to torch.initial_seed() (what torch.manual_seed
+    set), so runs stay reproducible; the rank offset is an odd 64-bit multiplier (distinct
+    streams for every rank)."""
+    if rank is None:
+        rank = dist.get_rank() if dist.is_initialized() else 0
+    if seed is None:
+        seed = torch.initial_seed()
+    g = torch.Generator(device=device)
+    g.manual_seed((int(seed) + 0x9E3779B97F4A7C15 * (int(rank) + 1)) % (1 << 63))
+    return g
+
+
 class GradBuffer:
     """Flat gradient storage for ``params`` (in order); ``views[i]`` has ``params[i]``'s shape.
     Every view starts on a 256-byte boundary (``ALIGN`` floats), so the vectorised kernels that

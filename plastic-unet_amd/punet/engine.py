@@ -47,6 +47,10 @@ class Trainer:
             trunk.gradbuf = self.gradbuf
             if self.distributed and overlap:
                 self.reducer = dp.BucketReducer(self.gradbuf, bucket_mb=bucket_mb, force=force_reduce)
+            if self.distributed and dist.get_world_size() > 1 and hasattr(trunk, "mask_gen") \
+                    and trunk.mask_gen is None:
+                # Dropout2d masks: independent per rank (the parameters are the broadcast ones)
+                trunk.mask_gen = dp.rank_generator(next(net.parameters()).device)
         self.overlapped_buckets = 0
         # HIP-graph step (one rank only: the overlapped all-reduce issues collectives from the host
         # during backward); eager warm-up steps first, then capture
@@ -109,8 +113,17 @@ class Trainer:
             self._graph_warm += 1
         return self._eager_step(x, t, hebb)
 
+    @staticmethod
+    def _sig(net, *ts):
+        return (net.training,) + tuple((tuple(a.shape), a.dtype, a.device) for a in ts)
+
     def _graph_step(self, x, t, hebb):
+        if self._graph is not None and self._sig(self.net, x, t, hebb) != self._gsig:
+            # copy_() would broadcast a different batch into the captured one, and an eval-mode
+            # call would replay the training graph: anything but the captured step runs eagerly
+            return self._eager_step(x, t, hebb)
         if self._graph is None:
+            self._gsig = self._sig(self.net, x, t, hebb)
             # capture right after an (eager) optimizer step: every packed operand is stale, so the
             # trunk's refresh launches are part of the graph and run on every replay
             self._sx = x.detach().clone()

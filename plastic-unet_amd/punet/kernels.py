@@ -403,6 +403,9 @@ def pack_weight(w, mode, k_pad, out=None, cgroup=0, dtype=torch.float32):
             # a U packed from the old weights must not outlive them: repacked in place with
             # Winograd off, then Winograd back on, igemm would otherwise run on the stale U
             del out._wino
+            # no Winograd path any more: the direct operand is the one igemm uses, refreshed
+            # every step like any other (trunk._Packs.refresh)
+            out._wino_only, out._direct_ok = False, True
     out._pack_spec = (mode, k_pad, cgroup)    # pack_weights() refreshes it in place
     return out
 

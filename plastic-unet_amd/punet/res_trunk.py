@@ -185,6 +185,8 @@ class ResTrunk:
         self.training = True
         self.gradbuf = None
         self.mask_fn = None      # (name, batch, channels, p) -> [B, C] scale; default: bernoulli
+        self.mask_gen = None     # torch.Generator for the bernoulli masks (None: torch's default);
+                                 # data-parallel Trainers set a per-rank one (punet.dp.rank_generator)
         self.fused_head = False  # as UNetpTrunk.fused_head
         self.debug = None
 
@@ -217,7 +219,8 @@ class ResTrunk:
     def _mask(self, name, B, C, p, device):
         if self.mask_fn is not None:
             return self.mask_fn(name, B, C, p)
-        return torch.empty(B, C, dtype=torch.float32, device=device).bernoulli_(1.0 - p).div_(1.0 - p)
+        return torch.empty(B, C, dtype=torch.float32, device=device).bernoulli_(
+            1.0 - p, generator=self.mask_gen).div_(1.0 - p)
 
     # ---------------------------------------------------------------------------- forward
     def _bn(self, P, key, z, relu, resid=None, save=None):

@@ -125,3 +125,34 @@ def test_bucket_reducer_two_ranks(tmp_path):
             want = sum(base * (r + 1) + 100 * i + step for r in range(world)) / world
             for r in range(world):
                 torch.testing.assert_close(got[r][i], want)
+
+
+def _gen_worker(rank, world, port, out_dir):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from punet import dp
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    torch.manual_seed(5)                     # every rank seeds identically (bench.py / train.py)
+    g = dp.rank_generator("cpu")
+    m = torch.empty(16, 64).bernoulli_(0.5, generator=g)
+    g2 = dp.rank_generator("cpu")            # same rank, same seed: the same stream
+    m2 = torch.empty(16, 64).bernoulli_(0.5, generator=g2)
+    torch.save({"m": m, "m2": m2}, os.path.join(out_dir, "gen%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_generator_decorrelates_dropout_masks(tmp_path):
+    """Dropout2d masks under DP: with the same torch.manual_seed on every rank
+    the per-rank generators draw different masks, reproducibly."""
+    world = 2
+    mp.spawn(_gen_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = [torch.load(os.path.join(tmp_path, "gen%d.pt" % r), weights_only=True) for r in range(world)]
+    for r in got:
+        assert torch.equal(r["m"], r["m2"])
+    assert not torch.equal(got[0]["m"], got[1]["m"])
+    # independent draws: about half of the mask entries differ between the ranks
+    frac = (got[0]["m"] != got[1]["m"]).float().mean().item()
+    assert 0.35 < frac < 0.65, frac
