@@ -530,6 +530,479 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ------------------------------------------------------------------ one wave per SIMD: wino4_x6_kernel
+// The same F(2x2,3x3) items (64 tiles x 64 output channels x a K range), products, U / V planes
+// and output-transform expression tree as wino_x6_kernel - bit-identical results - re-tiled for
+// one wave per SIMD: 4 waves, wave j owns position column j of every row i for the WHOLE 64 x 64
+// item (2 x 2 MFMA blocks per position: 4 rows x 4 blocks = 256 accumulators, AGPRs), one item
+// per block.
+// Why: wino_x6_kernel's 8 waves each run a 32 x 32 block per position, so every MFMA needs its
+// own U and V fragment (1 KB of LDS reads per MFMA; 96 KB per sub-stage on top of the 48 KB of U
+// DMA and V stores), and after each sub-stage barrier both waves of a SIMD first wait for their
+// LDS fragment reads.  Here a U fragment feeds 2 MFMAs and a V fragment 2 (24 KB of V reads per
+// sub-stage), U goes straight from L2 into registers one sub-stage ahead (no LDS-DMA), and the
+// sub-stages are software-pipelined so the matrix pipe does not wait for LDS after a barrier:
+//   * V is formed TWO sub-stages ahead into a 3-slot ring (3 x 24 KB): during sub-stage s the
+//     producer role (thread = tile tt, channel quad qq; its 4x4 window of 4 channels in 16 x f32x4)
+//     forms V(s+2), and every wave pre-reads its 6 fragments of V(s+1) - complete at barrier(s) -
+//     so the MFMAs of s+1 start right after barrier(s+1);
+//   * window rows of a chunk are reloaded as soon as the formation no longer reads them (row 2 of
+//     the next chunk in i = 0, rows 1 and 3 in i = 1, row 0 of the chunk after next in i = 2);
+//   * item end: s_py[j] = sum_i A^T[py][i] M[i][j] is lane-local; wave b then owns block b
+//     = (channel half b >> 1, tile half b & 1) and receives the other three columns' sums
+//     through the (then idle) V ring (3 rounds), forms Y = (s0 + s1) + s2, s1 - (s2 + s3) for
+//     both output rows and runs the batched float4 epilogue.
+#ifndef PU_W4_ABL
+#define PU_W4_ABL 0     // ablations (timing only, wrong results): 1 no MFMAs, 2 no V formation,
+                        // 4 no window loads, 5 no U loads
+#endif
+constexpr int W4_VH = 4 * 3 * 64 * 32;         // 24 KB: V of one sub-stage (4 xi x 3 planes x 64 tiles x 16)
+constexpr int W4_XF = 4 * 2 * 16 * 64;         // floats in one exchange round (32 KB, inside the V ring)
+
+template <bool FULL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino4_x6_kernel(const WinoParams w) {
+#pragma clang fp contract(off)
+    const IgemmParams& p = w.p;
+    __shared__ __attribute__((aligned(16))) unsigned char ldv[3 * W4_VH];
+    float* const xch = reinterpret_cast<float*>(ldv);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);   // position column j of this wave
+
+    // ---- the item (one per block, XCD-aware order)
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    const int per_split = w.gm * p.gn;
+    const int kz = item / per_split;
+    const int rest = item - kz * per_split;
+    const int nbk = rest / w.gm;
+    const int m_blk = (rest - nbk * w.gm) * WG_BM;
+    const int n_blk = nbk * WG_BN;
+    const int kc0 = kz * w.kc_per;
+    const int kc1 = min(p.C / 16, kc0 + w.kc_per);
+
+    // ---- producer role: tile tt of the item, channels 4qq .. 4qq+3 of each 16-channel chunk
+    const int tt = tid >> 2, qq = tid & 3;
+    const int cs = p.c0;
+    const int shift = p.Wi + 1;
+    const unsigned pixb = (unsigned)cs * 4u;
+    const float* a0 = p.src0 - (long long)shift * cs;
+    const float* a1 = (p.c1 ? p.src1 : p.src0) - (long long)shift * cs;
+    const int v_st = tt * 32 + (((qq >> 1) ^ ((tt >> 3) & 1)) * 16) + (qq & 1) * 8;
+    unsigned vrow[4];
+    bool c0ok, c3ok;
+    {
+        const int m = m_blk + tt;
+        int ty = 0, tx = 0, b = 0;
+        const bool mv = m < w.tiles;
+        if (mv) {
+            const int t2 = fdiv(m, w.dTw);
+            tx = m - t2 * (p.Wo >> 1);
+            b = fdiv(t2, w.dTh);
+            ty = t2 - b * (p.Ho >> 1);
+        }
+        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + qq * 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
+        c0ok = x0 >= 0;
+        c3ok = x0 + 3 < p.Wi;
+    }
+
+    // ---- MFMA role: V rows 32 tb + (lane & 31) of position j, swizzled half (as wino_x6_kernel)
+    const int rd_sw = (((lane >> 5) ^ ((lane >> 3) & 1)) * 16);
+    const int v_rd = (lane & 31) * 32 + rd_sw + wj * 3 * 2048;
+    // U fragment (n = 32 cb + (lane & 31), k half lane >> 5) of (chunk, xi, plane): 1 KB per wave
+    const unsigned u_row = (unsigned)p.N * 32u;
+    const unsigned u_lane = (unsigned)(lane & 31) * 32u + (unsigned)(lane >> 5) * 16u;
+
+    f32x4 d[16];                 // window [row][col] of 4 channels
+    f32x16 acc[4][2][2];         // [i][cb][tb]
+    bf16x8_t fu[2][2][3];        // U fragments [slot][cb][plane], one sub-stage ahead
+    bf16x8_t fv[2][2][3];        // V fragments [slot][tb][plane], one sub-stage ahead
+
+    auto load_row = [&](int kc, int rr) {
+        if (PU_W4_ABL == 4) {
+#pragma unroll
+            for (int ss = 0; ss < 4; ++ss) d[rr * 4 + ss] = f32x4{1.f + rr, 0.5f * ss, 0.25f, (float)kc};
+            return;
+        }
+        const int c = kc * 16;
+        const bool second = c >= p.c0;
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(second ? a1 : a0, kc < kc1 ? w.a_bytes : 0u);
+        const unsigned cb = (unsigned)((second ? c - p.c0 : c) * 4);
+#pragma unroll
+        for (int ss = 0; ss < 4; ++ss) {
+            unsigned vo = vrow[rr];
+            if (ss == 0) vo = c0ok ? vo : LEAN_OOB;
+            if (ss == 3) vo = c3ok ? vo : LEAN_OOB;
+            const unsigned soff = __builtin_amdgcn_readfirstlane(cb + ss * pixb);
+            d[rr * 4 + ss] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, 0));
+        }
+    };
+    // U fragments of position (i, wj) of chunk kc into register slot sl (zeros past the item's chunks)
+    auto load_u = [&](int kc, int i, auto sl_c) {
+        constexpr int sl = decltype(sl_c)::value;
+        if (PU_W4_ABL == 5) {
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) fu[sl][cb][pl] = __builtin_bit_cast(bf16x8_t, u32x4{(unsigned)kc, (unsigned)i, 0u, 1u});
+            return;
+        }
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(w.U, kc < kc1 ? w.u_bytes : 0u);
+        const unsigned sb = (unsigned)((kc * 16 + 4 * i + wj) * 3) * u_row + (unsigned)(n_blk * 32);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                fu[sl][cb][pl] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                    r, u_lane + (unsigned)cb * 1024u, __builtin_amdgcn_readfirstlane(sb + pl * u_row), 0));
+    };
+    // this wave's V fragments (position wj, 2 tile halves x 3 planes) of the V slot at byte offset so
+    auto read_v = [&](unsigned so, auto sl_c) {
+        constexpr int sl = decltype(sl_c)::value;
+        const unsigned char* vb = ldv + so + v_rd;
+#pragma unroll
+        for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                fv[sl][tb][pl] = *reinterpret_cast<const bf16x8_t*>(vb + tb * 1024 + pl * 2048);
+    };
+    // V of row f (4 positions) for this thread's tile and 4 channels -> hi / mid / lo planes
+    auto make_v = [&](auto f_c, unsigned so) {
+        constexpr int f = decltype(f_c)::value;
+        if (PU_W4_ABL == 2) return;
+        f32x4 t[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            if constexpr (f == 0) t[s2] = d[s2] - d[8 + s2];
+            else if constexpr (f == 1) t[s2] = d[4 + s2] + d[8 + s2];
+            else if constexpr (f == 2) t[s2] = d[8 + s2] - d[4 + s2];
+            else t[s2] = d[4 + s2] - d[12 + s2];
+        }
+        const f32x4 v[4] = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+        unsigned char* base = ldv + so + v_st;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+            bf16x8_t h, m, l;
+            split3_pairs(v[2 * jp], v[2 * jp + 1], h, m, l);
+            const u32x4 pv[3] = {__builtin_bit_cast(u32x4, h), __builtin_bit_cast(u32x4, m), __builtin_bit_cast(u32x4, l)};
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                *reinterpret_cast<u32x2*>(base + ((2 * jp) * 3 + pl) * 2048) = u32x2{pv[pl][0], pv[pl][1]};
+                *reinterpret_cast<u32x2*>(base + ((2 * jp + 1) * 3 + pl) * 2048) = u32x2{pv[pl][2], pv[pl][3]};
+            }
+        }
+    };
+    // the 24 MFMAs of position (i, wj): U slot su x V slot sv, the 6 products of each of the
+    // 4 blocks in wino_x6_kernel's order; the item's first chunk starts from C = 0
+    auto mma = [&](auto i_c, auto sl_c, auto first_c) {
+        constexpr int i = decltype(i_c)::value;
+        constexpr int sl = decltype(sl_c)::value;
+        constexpr bool FIRST = decltype(first_c)::value;
+        if (PU_W4_ABL == 1) {
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int tb = 0; tb < 2; ++tb)
+                    acc[i][cb][tb][0] += __builtin_bit_cast(float, __builtin_shufflevector(fu[sl][cb][0], fv[sl][tb][1], 0, 9));
+            return;
+        }
+        constexpr int PU[6] = {1, 2, 0, 1, 0, 0}, PV[6] = {1, 0, 2, 0, 1, 0};
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int tb = 0; tb < 2; ++tb)
+                    acc[i][cb][tb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        fu[sl][cb][PU[e]], fv[sl][tb][PV[e]], (FIRST && e == 0) ? f32x16{} : acc[i][cb][tb], 0, 0, 0);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+
+    // V ring: V(s) in slot s % 3 (byte offset sv), V(s+1) / V(s+2) in the next two
+    unsigned sv = 0;
+    auto slot_after = [](unsigned so, int k) -> unsigned {
+        unsigned r = so + (unsigned)k * W4_VH;
+        return r >= 3u * W4_VH ? r - 3u * W4_VH : r;
+    };
+
+    // sub-stage (kc, i) = s.  At barrier(s) every wave has finished s-1, so V(s+1) (formed during
+    // s-1) is complete and V(s-1)'s slot - its fragments were pre-read during s-2 - is free for
+    // V(s+2).  The MFMAs use the V fragments read during s-1 and the U fragments issued during s-1.
+    auto sub = [&](int kc, auto i_c, auto first_c) {
+        constexpr int i = decltype(i_c)::value;
+        constexpr int F = (i + 2) & 3;                 // the row formed now (chunk kc, or kc+1 for i >= 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // pin this sub-stage's fragments (U issued and V read during s-1) here: the MFMAs would
+        // otherwise be hoisted across barrier(s) into sub-stage s-1
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) asm volatile("" : "+v"(fu[i & 1][k][pl]), "+v"(fv[i & 1][k][pl]));
+        // pin the window rows this formation reads (F = 2: rows 1, 2; 3: 1, 3; 0: 0, 2; 1: 1, 2):
+        // the formation is pure VALU and would otherwise be hoisted across the barriers
+        constexpr int RA = F == 0 ? 0 : 1, RB = F == 3 ? 3 : 2;
+#pragma unroll
+        for (int ss = 0; ss < 4; ++ss) asm volatile("" : "+v"(d[RA * 4 + ss]), "+v"(d[RB * 4 + ss]));
+        read_v(slot_after(sv, 1), std::integral_constant<int, (i + 1) & 1>{});
+        if constexpr (i < 3) load_u(kc, i + 1, std::integral_constant<int, (i + 1) & 1>{});
+        else load_u(kc + 1, 0, I0{});
+        mma(i_c, std::integral_constant<int, i & 1>{}, first_c);
+        // pin this sub-stage's MFMAs here: they are pure, and the selection DAG of the unrolled
+        // chunk would otherwise float them past the following barriers
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int tb = 0; tb < 2; ++tb) asm volatile("" : "+a"(acc[i][cb][tb]));
+        make_v(std::integral_constant<int, F>{}, slot_after(sv, 2));
+        if constexpr (i == 0) load_row(kc + 1, 2);
+        if constexpr (i == 1) {
+            load_row(kc + 1, 1);
+            load_row(kc + 1, 3);
+        }
+        if constexpr (i == 2) load_row(kc + 2, 0);
+        sv = slot_after(sv, 1);
+#if PU_W4_ABL == 0 && !PU_NO_ILV
+        // issue order: V(s+1) fragment reads, U(s+1), then the 24 MFMAs with the formation of
+        // V(s+2) in their shadow (~4 VALU per MFMA, a plane store every other one)
+        // (the 12 plane stores are merged into 6 ds_write2st64 before scheduling)
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
+#pragma unroll
+        for (int q = 0; q < 24; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            if ((q & 3) == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);
+#endif
+    };
+
+    // prologue: the first chunk's window, U of sub-stage 0, V(0) and V(1) into slots 0 / 1, the
+    // next chunk's row 0 (row 0 of the first chunk is dead after V(0)), V(0)'s fragments
+    load_row(kc0, 0);
+    load_row(kc0, 1);
+    load_row(kc0, 2);
+    load_row(kc0, 3);
+    load_u(kc0, 0, I0{});
+    make_v(I0{}, 0u);
+    make_v(I1{}, (unsigned)W4_VH);
+    load_row(kc0 + 1, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_v(0u, I0{});
+
+    using BT = std::true_type;
+    using BF = std::false_type;
+    // the item's first chunk starts every accumulator from C = 0 (no zeroing pass); every item
+    // has >= 2 chunks (wino_ok: C % 32 == 0, even chunks per K split)
+    sub(kc0, std::integral_constant<int, 0>{}, BT{});
+    sub(kc0, std::integral_constant<int, 1>{}, BT{});
+    sub(kc0, std::integral_constant<int, 2>{}, BT{});
+    sub(kc0, std::integral_constant<int, 3>{}, BT{});
+    for (int kc = kc0 + 1; kc < kc1; ++kc) {
+        sub(kc, std::integral_constant<int, 0>{}, BF{});
+        sub(kc, std::integral_constant<int, 1>{}, BF{});
+        sub(kc, std::integral_constant<int, 2>{}, BF{});
+        sub(kc, std::integral_constant<int, 3>{}, BF{});
+    }
+    // every wave is done reading the V ring (the exchange reuses it)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // ---- output transform.  Column sums s_py[j] (lane-local, wino_x6_kernel's order):
+    // s_0 = (M0 + M1) + M2, s_1 = (M1 - M2) - M3.  Wave b owns block b = (cb, tb) = (b >> 1,
+    // b & 1); in round r wave j sends block (j + r) & 3 and receives block b from wave (b - r) & 3.
+    // Specialised per wave (a uniform switch) so every register index is static; the column sums
+    // live in accumulator registers whose products are consumed (the own column in acc[0 / 1][J],
+    // the column received in round r in acc[0 / 1][block sent in round r]); Y in acc[3][py][px].
+    auto xform = [&](auto j_c) {
+        constexpr int J = decltype(j_c)::value;
+#define W4A(i, b) acc[i][(b) >> 1][(b) & 1]
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const float s0 = W4A(0, J)[e] + W4A(1, J)[e] + W4A(2, J)[e];
+            const float s1 = W4A(1, J)[e] - W4A(2, J)[e] - W4A(3, J)[e];
+            W4A(0, J)[e] = s0;
+            W4A(1, J)[e] = s1;
+        }
+        float* xs = xch + J * (2 * 16 * 64);
+        auto round = [&](auto r_c) {
+            constexpr int R = decltype(r_c)::value;
+            constexpr int SB = (J + R) & 3, FROM = (J - R) & 3;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                xs[e * 64 + lane] = W4A(0, SB)[e] + W4A(1, SB)[e] + W4A(2, SB)[e];
+                xs[(16 + e) * 64 + lane] = W4A(1, SB)[e] - W4A(2, SB)[e] - W4A(3, SB)[e];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const float* xr = xch + FROM * (2 * 16 * 64);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                W4A(0, SB)[e] = xr[e * 64 + lane];
+                W4A(1, SB)[e] = xr[(16 + e) * 64 + lane];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        };
+        round(std::integral_constant<int, 1>{});
+        round(std::integral_constant<int, 2>{});
+        round(std::integral_constant<int, 3>{});
+        // column j was received in round r = (J - j) & 3 and sits in block (J + r) & 3 (r = 0: own)
+        constexpr int B0 = (J + ((J - 0) & 3)) & 3, B1 = (J + ((J - 1) & 3)) & 3;
+        constexpr int B2 = (J + ((J - 2) & 3)) & 3, B3 = (J + ((J - 3) & 3)) & 3;
+#pragma unroll
+        for (int py = 0; py < 2; ++py)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const float c0 = W4A(py, B0)[e], c1 = W4A(py, B1)[e], c2 = W4A(py, B2)[e], c3 = W4A(py, B3)[e];
+                acc[3][py][0][e] = (c0 + c1) + c2;      // Y[py][0] = (s0 + s1) + s2
+                acc[3][py][1][e] = c1 - (c2 + c3);      // Y[py][1] = s1 - (s2 + s3)
+            }
+#undef W4A
+    };
+    switch (wj) {
+        case 0: xform(std::integral_constant<int, 0>{}); break;
+        case 1: xform(std::integral_constant<int, 1>{}); break;
+        case 2: xform(std::integral_constant<int, 2>{}); break;
+        default: xform(std::integral_constant<int, 3>{}); break;
+    }
+
+    const int cbo = wj >> 1, tbo = wj & 1;
+    const int e_m = m_blk + 32 * tbo + (lane & 31), e_n = n_blk + 32 * cbo + 4 * (lane >> 5);
+    const bool e_ok = e_m < w.tiles;
+    const int em = e_ok ? e_m : 0;
+    const int t2 = fdiv(em, w.dTw);
+    const int tx = em - t2 * (p.Wo >> 1);
+    const int b = fdiv(t2, w.dTh);
+    const int ty = t2 - b * (p.Ho >> 1);
+    const long long pix00 = ((long long)b * p.Ho + 2 * ty) * p.Wo + 2 * tx;
+    auto yv = [&](int py, int o, int g) {
+        return f32x4{acc[3][py][o][4 * g], acc[3][py][o][4 * g + 1], acc[3][py][o][4 * g + 2], acc[3][py][o][4 * g + 3]};
+    };
+    if (p.ksplit == 1) {
+        // wino_x6_kernel's batched float4 epilogue for both output rows: operand loads first,
+        // then the stores
+        const bool first = n_blk < p.n0;
+        const int ld = first ? p.n0 : p.N - p.n0;
+        float* dst = first ? p.dst0 : p.dst1;
+        const float* msk = first ? p.mask0 : p.mask1;
+        const bool relu = p.flags & PU_EPI_RELU, accum = p.flags & PU_EPI_ACCUM;
+        constexpr unsigned RANGE = 0x7fffffffu;
+        const __amdgpu_buffer_rsrc_t r_dst = uniform_rsrc(dst, RANGE);
+        const __amdgpu_buffer_rsrc_t r_msk = uniform_rsrc(msk, msk ? RANGE : 0u);
+        const __amdgpu_buffer_rsrc_t r_bias = uniform_rsrc(p.bias, p.bias ? RANGE : 0u);
+        const unsigned o_px = e_ok ? (unsigned)(pix00 * ld + e_n - (first ? 0 : p.n0)) * 4u : LEAN_OOB;
+        const unsigned o_col = (unsigned)ld * 4u;                  // next pixel in x
+        const unsigned o_row = (unsigned)p.Wo * (unsigned)ld * 4u;  // next pixel row
+        if constexpr (!FULL) {
+            // bias (+ ReLU) and / or a ReLU mask (the UNetp layers): the bias and the first output
+            // row's masks, that row's stores, then the second row
+            f32x4 bv[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) bv[g] = epi_ld4(r_bias, (unsigned)(e_n + 8 * g) * 4u);
+#pragma unroll
+            for (int py = 0; py < 2; ++py) {
+                f32x4 mv[4][2];
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) mv[g][o] = epi_ld4(r_msk, o_px + py * o_row + o * o_col + 32u * g);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    asm volatile("" :: "v"(bv[g]));
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) asm volatile("" :: "v"(mv[g][o]));
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) {
+                        f32x4 v = yv(py, o, g);
+                        if (p.bias) v += bv[g];
+                        if (relu) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                        }
+                        if (msk) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) if (!(mv[g][o][e] > 0.f)) v[e] = 0.f;
+                        }
+                        epi_st4(r_dst, o_px + py * o_row + o * o_col + 32u * g, v);
+                    }
+            }
+        } else {
+            // every epilogue operand (residual, channel scale, accumulate), one output row at a time
+            const __amdgpu_buffer_rsrc_t r_acc = uniform_rsrc(dst, accum ? RANGE : 0u);
+            const __amdgpu_buffer_rsrc_t r_res = uniform_rsrc(p.resid, p.resid ? RANGE : 0u);
+            const __amdgpu_buffer_rsrc_t r_cs = uniform_rsrc(p.cscale, p.cscale ? RANGE : 0u);
+            const unsigned o_cs = (unsigned)(b * p.cs_ld + e_n) * 4u;
+#pragma unroll
+            for (int py = 0; py < 2; ++py) {
+                f32x4 bv[4], sv4[4], rv[4][2], mv[4][2], av[4][2];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    bv[g] = epi_ld4(r_bias, (unsigned)(e_n + 8 * g) * 4u);
+                    sv4[g] = epi_ld4(r_cs, o_cs + 32u * g);
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) {
+                        const unsigned off = o_px + py * o_row + o * o_col + 32u * g;
+                        rv[g][o] = epi_ld4(r_res, off);
+                        mv[g][o] = epi_ld4(r_msk, off);
+                        av[g][o] = epi_ld4(r_acc, off);
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    asm volatile("" :: "v"(bv[g]), "v"(sv4[g]));
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) asm volatile("" :: "v"(rv[g][o]), "v"(mv[g][o]), "v"(av[g][o]));
+                }
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) {
+                        f32x4 v = yv(py, o, g);
+                        if (p.bias) v += bv[g];
+                        if (p.resid) v += rv[g][o];
+                        if (relu) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                        }
+                        if (msk) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) if (!(mv[g][o][e] > 0.f)) v[e] = 0.f;
+                        }
+                        if (p.cscale) v *= sv4[g];
+                        if (accum) v += av[g][o];
+                        epi_st4(r_dst, o_px + py * o_row + o * o_col + 32u * g, v);
+                    }
+            }
+        }
+    } else if (e_ok) {
+        float* part = p.part + (long long)kz * p.M * p.N + pix00 * p.N + e_n;
+#pragma unroll
+        for (int py = 0; py < 2; ++py)
+#pragma unroll
+            for (int o = 0; o < 2; ++o)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    *reinterpret_cast<f32x4*>(part + ((long long)py * p.Wo + o) * p.N + 8 * g) = yv(py, o, g);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ------------------------------------------------------------------ 128-channel Winograd items
 // wino128_x6_kernel: the same F(2x2,3x3) arithmetic, products and output transform as
 // wino_x6_kernel, with items of 32 tiles x 128 output channels instead of 64 x 64, so each V
@@ -1092,6 +1565,16 @@ static bool wino_persist() {
     return on;
 }
 
+// 64 x 64 items on one wave per SIMD (wino4_x6_kernel, bit-identical to wino_x6_kernel; default):
+// PU_WINO4=0 keeps the 8-wave kernel (A/B runs, profiles/r06_experiments/wino4_ab.txt)
+static bool wino4_on() {
+    static const bool on = [] {
+        const char* e = getenv("PU_WINO4");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     WinoParams w;
     w.p = p;
@@ -1119,6 +1602,13 @@ int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
             hipLaunchKernelGGL(wino128_x6_kernel<true>, dim3(256), dim3(512), 0, s, w);
         else
             hipLaunchKernelGGL(wino128_x6_kernel<false>, dim3((unsigned)items), dim3(512), 0, s, w);
+        return ks;
+    }
+    if (wino4_on()) {
+        // one item per block (the pipelined kernel keeps the next chunks' rows in flight per item)
+        const bool full = p.resid || p.cscale || (p.flags & PU_EPI_ACCUM);
+        if (full) hipLaunchKernelGGL(wino4_x6_kernel<true>, dim3((unsigned)items), dim3(256), 0, s, w);
+        else hipLaunchKernelGGL(wino4_x6_kernel<false>, dim3((unsigned)items), dim3(256), 0, s, w);
         return ks;
     }
     if (wino_persist() && items > 256)

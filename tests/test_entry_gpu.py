@@ -142,3 +142,55 @@ def test_streamed_batches_train_identically_to_resident(tmp_path):
     assert res[0][0] == res[1][0]
     for k in res[0][1]:
         assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
+def test_train_c1_config_against_oracle(tmp_path):
+    """Config C1 (BASELINE configs[0]): UNetp depth 4 / base 16, Hebb rule, 1x128x128, batch 2 -
+    train.train() on the HIP path against the CPU oracle running the same batched steps (per-slot
+    traces carried, Adam + StepLR per step, train.py:91-112): 2 epochs x 2 steps.  Losses within
+    1e-4 (north_star); parameters: the updates agree in direction (cosine) and per coordinate
+    except where Adam's first step divides a rounding-level gradient by itself (sign flips)."""
+    import train
+    torch.manual_seed(41)
+    ref = oracle.RefUNetp(1, 1, rule="hebb", nbf=128, depth=4, base_ch=16)
+    net = UNetp(1, 1, DEV, rule="hebb", nbf=128, depth=4, base_ch=16)
+    net.load_state_dict(ref.state_dict())
+    init = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    g = np.random.RandomState(41)
+    X = g.rand(4, 1, 128, 128).astype(np.float32)
+    Y = (g.rand(4, 1, 128, 128) > 0.5).astype(np.float32)
+    lr, steplr = 3e-4, 3
+    params = {"out_dir": str(tmp_path), "device": DEV, "epochs": 2, "stop_time": -1, "lr": lr,
+              "val_every": 100, "save_every": 100, "rollout": 50000, "gamma": 0.666, "steplr": steplr,
+              "debug": False, "batch_size": 2}
+    losses = train.train(net, X, X[:2], Y, Y[:2], params)[0]
+    # the oracle: the same two batches per epoch, traces zeroed per epoch (train.py:88)
+    opt = oracle.ref_adam(ref.parameters(), lr)
+    sch = oracle.ref_steplr(opt, steplr)
+    ref_losses = []
+    for _ in range(2):
+        hebb = ref.initialZeroHebb(2)
+        for lo in (0, 2):
+            x = torch.from_numpy(X[lo:lo + 2])
+            t = torch.from_numpy(Y[lo:lo + 2]).reshape(2, -1)
+            loss, _, hebb = oracle.ref_train_step(ref, opt, sch, x, t, hebb)
+            ref_losses.append(loss.item())
+    assert len(losses) == 4
+    np.testing.assert_allclose(losses, ref_losses, rtol=1e-4)
+    flips = total = 0
+    for k, v in net.state_dict().items():
+        if k not in init or not v.dtype.is_floating_point:
+            continue
+        du = (v.cpu() - init[k]).double()
+        dr = (ref.state_dict()[k] - init[k]).double()
+        flips += int(((du - dr).abs() > 0.25 * lr).sum())
+        total += du.numel()
+    gu = torch.cat([(v.cpu() - init[k]).double().reshape(-1) for k, v in net.state_dict().items()
+                    if k in init and v.dtype.is_floating_point])
+    gr = torch.cat([(ref.state_dict()[k] - init[k]).double().reshape(-1) for k in net.state_dict()
+                    if k in init and net.state_dict()[k].dtype.is_floating_point])
+    cos = float(gu @ gr / (gu.norm() * gr.norm()))
+    print("C1 train: losses %s vs %s; update cosine %.6f; %d / %d coordinates apart by > lr/4"
+          % (losses, ref_losses, cos, flips, total))
+    assert cos > 0.999
+    assert flips <= 0.005 * total

@@ -176,7 +176,7 @@ def test_wino_persistent_equals_one_item_per_block(tmp_path):
     out = {}
     for persist in ("1", "0"):
         f = str(tmp_path / ("p%s.pt" % persist))
-        env = dict(os.environ, PU_WINO_PERSIST=persist, PU_WINO="1")
+        env = dict(os.environ, PU_WINO_PERSIST=persist, PU_WINO="1", PU_WINO4="0")   # the 8-wave kernel's modes
         r = subprocess.run([sys.executable, "-c", _PERSIST_SCRIPT, f, root], env=env, capture_output=True,
                            text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
@@ -267,3 +267,66 @@ def test_wino128_bit_identical_to_64_channel_items(tmp_path):
             assert (a is None) == (b is None), k
             if a is not None:
                 assert torch.equal(a, b), k
+
+
+_W4_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from punet import kernels as K, trunk as T
+out = {}
+for (B, H, W, c0, c1, N) in [(2, 16, 16, 64, 0, 64), (3, 10, 14, 128, 0, 128), (2, 8, 8, 64, 64, 64),
+                             (1, 32, 16, 128, 0, 192), (4, 8, 8, 512, 0, 512), (2, 16, 16, 256, 256, 256),
+                             (1, 2, 2, 32, 0, 64), (5, 128, 128, 64, 0, 64), (3, 96, 80, 128, 0, 192),
+                             (2, 24, 24, 128, 128, 128)]:
+    g = torch.Generator().manual_seed(B + H + W + c0 + c1 + N)
+    C = c0 + c1
+    x = torch.randn(B, H, W, C, generator=g).relu().cuda()
+    w = (torch.randn(N, C, 3, 3, generator=g) * 0.05).cuda()
+    b = torch.randn(N, generator=g).cuda()
+    dz = torch.randn(B, H, W, N, generator=g).cuda()
+    r = torch.randn(B, H, W, N, generator=g).cuda()
+    a0 = torch.randn(B, H, W, N, generator=g).cuda()
+    pk = T._Packs()
+    x0, x1 = (x[..., :c0].contiguous(), x[..., c0:].contiguous()) if c1 else (x, None)
+    y = T.conv3x3(x0, w, b, pk, x1=x1, relu=True)
+    d0, d1 = T.conv3x3_dgrad(dz, w, pk, split=c0 if c1 else None, mask0=x0, mask1=x1)
+    res = [y.cpu(), d0.cpu(), None if d1 is None else d1.cpu()]
+    if not c1:     # the general epilogue: residual + ReLU, accumulate
+        k_pad = K.round16(9 * C)
+        packed = pk.get(w, 0, k_pad, K.cgroup_for(C))
+        o1 = torch.empty(B, H, W, N, device="cuda")
+        K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=x, c0=C, weight=packed,
+                k_pad=k_pad, n=N, bias=b, dst0=o1, relu=True, resid=r, cgroup=K.cgroup_for(C))
+        o2 = a0.clone()
+        K.igemm(batch=B, in_hw=(H, W), out_hw=(H, W), k=3, stride=1, pad=1, src0=x, c0=C, weight=packed,
+                k_pad=k_pad, n=N, dst0=o2, accum=True, cgroup=K.cgroup_for(C))
+        res += [o1.cpu(), o2.cpu()]
+    out[(B, H, W, c0, c1, N)] = res
+torch.save(out, sys.argv[1])
+"""
+
+
+def test_wino4_bit_identical_to_8_wave_kernel(tmp_path):
+    """wino4_x6_kernel (one wave per SIMD, 2 x 2 MFMA blocks per position, U from L2 into
+    registers) and wino_x6_kernel (PU_WINO4=0; read once per process - two child processes) form
+    every accumulator from the same U / V planes in the same product order and run the same
+    output-transform expression tree: forward, data gradient (masks, concat split), residual and
+    accumulate epilogues bitwise equal - one and many items per block, split-K, concat sources,
+    ragged tile blocks."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plastic-unet_amd")
+    res = {}
+    for on in ("1", "0"):
+        f = str(tmp_path / ("w%s.pt" % on))
+        env = dict(os.environ, PU_WINO4=on, PU_WINO="1")
+        r = subprocess.run([sys.executable, "-c", _W4_SCRIPT, f, root], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[on] = torch.load(f, weights_only=True)
+    for k in res["1"]:
+        for i, (a, b) in enumerate(zip(res["1"][k], res["0"][k])):
+            assert (a is None) == (b is None), k
+            if a is not None:
+                assert torch.equal(a, b), (k, i, (a - b).abs().max().item())
