@@ -559,10 +559,20 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 constexpr int W4_VH = 4 * 3 * 64 * 32;         // 24 KB: V of one sub-stage (4 xi x 3 planes x 64 tiles x 16)
 constexpr int W4_XF = 4 * 2 * 16 * 64;         // floats in one exchange round (32 KB, inside the V ring)
 
-template <bool FULL>
+template <bool FULL, int NCB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino4_x6_kernel(const WinoParams w) {
 #pragma clang fp contract(off)
     const IgemmParams& p = w.p;
+    // item shape: NCB 32-channel blocks x NTB 32-tile blocks (2 x 2: 64 x 64, or 4 x 1: 128
+    // channels x 32 tiles - half the V formation and window loads per MFMA, twice the U)
+    constexpr int NTB = 4 / NCB, BM = 32 * NTB, BN = 32 * NCB;
+    constexpr int TPT = 256 / BM, CPT = 16 / TPT;       // producer threads per tile, channels per thread
+    constexpr int PS = BM * 32;                          // bytes per (position, plane) block of a V slot
+    constexpr int VS = 12 * PS;                          // one V slot
+    typedef float wv_t __attribute__((ext_vector_type(CPT)));
+    // U fragments UA sub-stages ahead in a USL-slot register ring (2 ahead for 64-channel items;
+    // the 128-channel items' 12 fragments per sub-stage only fit one ahead)
+    constexpr int UA = NCB == 2 ? 2 : 1, USL = 2 * UA;
     __shared__ __attribute__((aligned(16))) unsigned char ldv[3 * W4_VH];
     float* const xch = reinterpret_cast<float*>(ldv);
 
@@ -576,19 +586,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int kz = item / per_split;
     const int rest = item - kz * per_split;
     const int nbk = rest / w.gm;
-    const int m_blk = (rest - nbk * w.gm) * WG_BM;
-    const int n_blk = nbk * WG_BN;
+    const int m_blk = (rest - nbk * w.gm) * BM;
+    const int n_blk = nbk * BN;
     const int kc0 = kz * w.kc_per;
     const int kc1 = min(p.C / 16, kc0 + w.kc_per);
 
-    // ---- producer role: tile tt of the item, channels 4qq .. 4qq+3 of each 16-channel chunk
-    const int tt = tid >> 2, qq = tid & 3;
+    // ---- producer role: tile tt of the item, channels CPT qq .. CPT qq + CPT-1 of each 16-channel chunk
+    const int tt = tid / TPT, qq = tid % TPT;
     const int cs = p.c0;
     const int shift = p.Wi + 1;
     const unsigned pixb = (unsigned)cs * 4u;
     const float* a0 = p.src0 - (long long)shift * cs;
     const float* a1 = (p.c1 ? p.src1 : p.src0) - (long long)shift * cs;
-    const int v_st = tt * 32 + (((qq >> 1) ^ ((tt >> 3) & 1)) * 16) + (qq & 1) * 8;
+    const int v_st = tt * 32 + ((((CPT * qq * 2) >> 4) ^ ((tt >> 3) & 1)) * 16) + ((CPT * qq * 2) & 15);
     unsigned vrow[4];
     bool c0ok, c3ok;
     {
@@ -602,7 +612,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             ty = t2 - b * (p.Ho >> 1);
         }
         const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
-        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + qq * 16);
+        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs * 4 + qq * CPT * 4);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             vrow[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi * cs * 4) : LEAN_OOB;
@@ -612,20 +622,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     // ---- MFMA role: V rows 32 tb + (lane & 31) of position j, swizzled half (as wino_x6_kernel)
     const int rd_sw = (((lane >> 5) ^ ((lane >> 3) & 1)) * 16);
-    const int v_rd = (lane & 31) * 32 + rd_sw + wj * 3 * 2048;
+    const int v_rd = (lane & 31) * 32 + rd_sw + wj * 3 * PS;
     // U fragment (n = 32 cb + (lane & 31), k half lane >> 5) of (chunk, xi, plane): 1 KB per wave
     const unsigned u_row = (unsigned)p.N * 32u;
     const unsigned u_lane = (unsigned)(lane & 31) * 32u + (unsigned)(lane >> 5) * 16u;
 
-    f32x4 d[16];                 // window [row][col] of 4 channels
-    f32x16 acc[4][2][2];         // [i][cb][tb]
-    bf16x8_t fu[2][2][3];        // U fragments [slot][cb][plane], one sub-stage ahead
-    bf16x8_t fv[2][2][3];        // V fragments [slot][tb][plane], one sub-stage ahead
+    wv_t d[16];                  // window [row][col] of CPT channels
+    f32x16 acc[4][NCB][NTB];     // [i][cb][tb]
+    bf16x8_t fu[USL][NCB][3];    // U fragments [slot][cb][plane], UA sub-stages ahead
+    bf16x8_t fv[2][NTB][3];      // V fragments [slot][tb][plane], one sub-stage ahead
 
     auto load_row = [&](int kc, int rr) {
         if (PU_W4_ABL == 4) {
 #pragma unroll
-            for (int ss = 0; ss < 4; ++ss) d[rr * 4 + ss] = f32x4{1.f + rr, 0.5f * ss, 0.25f, (float)kc};
+            for (int ss = 0; ss < 4; ++ss) d[rr * 4 + ss] = wv_t(1.f + rr + 0.5f * ss + 0.25f * kc);
             return;
         }
         const int c = kc * 16;
@@ -638,7 +648,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             if (ss == 0) vo = c0ok ? vo : LEAN_OOB;
             if (ss == 3) vo = c3ok ? vo : LEAN_OOB;
             const unsigned soff = __builtin_amdgcn_readfirstlane(cb + ss * pixb);
-            d[rr * 4 + ss] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, 0));
+            if constexpr (CPT == 4)
+                d[rr * 4 + ss] = __builtin_bit_cast(wv_t, __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, 0));
+            else
+                d[rr * 4 + ss] = __builtin_bit_cast(wv_t, __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0));
         }
     };
     // U fragments of position (i, wj) of chunk kc into register slot sl (zeros past the item's chunks)
@@ -646,7 +659,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         constexpr int sl = decltype(sl_c)::value;
         if (PU_W4_ABL == 5) {
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb)
+            for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) fu[sl][cb][pl] = __builtin_bit_cast(bf16x8_t, u32x4{(unsigned)kc, (unsigned)i, 0u, 1u});
             return;
@@ -654,7 +667,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const __amdgpu_buffer_rsrc_t r = uniform_rsrc(w.U, kc < kc1 ? w.u_bytes : 0u);
         const unsigned sb = (unsigned)((kc * 16 + 4 * i + wj) * 3) * u_row + (unsigned)(n_blk * 32);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
+        for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
                 fu[sl][cb][pl] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
@@ -665,16 +678,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         constexpr int sl = decltype(sl_c)::value;
         const unsigned char* vb = ldv + so + v_rd;
 #pragma unroll
-        for (int tb = 0; tb < 2; ++tb)
+        for (int tb = 0; tb < NTB; ++tb)
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
-                fv[sl][tb][pl] = *reinterpret_cast<const bf16x8_t*>(vb + tb * 1024 + pl * 2048);
+                fv[sl][tb][pl] = *reinterpret_cast<const bf16x8_t*>(vb + tb * 1024 + pl * PS);
     };
     // V of row f (4 positions) for this thread's tile and 4 channels -> hi / mid / lo planes
     auto make_v = [&](auto f_c, unsigned so) {
         constexpr int f = decltype(f_c)::value;
         if (PU_W4_ABL == 2) return;
-        f32x4 t[4];
+        wv_t t[4];
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
             if constexpr (f == 0) t[s2] = d[s2] - d[8 + s2];
@@ -682,43 +695,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             else if constexpr (f == 2) t[s2] = d[8 + s2] - d[4 + s2];
             else t[s2] = d[4 + s2] - d[12 + s2];
         }
-        const f32x4 v[4] = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+        const wv_t v[4] = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
         unsigned char* base = ldv + so + v_st;
+        if constexpr (CPT == 4) {
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
+            for (int jp = 0; jp < 2; ++jp) {
+                bf16x8_t h, m, l;
+                split3_pairs(v[2 * jp], v[2 * jp + 1], h, m, l);
+                const u32x4 pv[3] = {__builtin_bit_cast(u32x4, h), __builtin_bit_cast(u32x4, m), __builtin_bit_cast(u32x4, l)};
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) {
+                    *reinterpret_cast<u32x2*>(base + ((2 * jp) * 3 + pl) * PS) = u32x2{pv[pl][0], pv[pl][1]};
+                    *reinterpret_cast<u32x2*>(base + ((2 * jp + 1) * 3 + pl) * PS) = u32x2{pv[pl][2], pv[pl][3]};
+                }
+            }
+        } else {
             bf16x8_t h, m, l;
-            split3_pairs(v[2 * jp], v[2 * jp + 1], h, m, l);
+            split3_pairs(f32x4{v[0][0], v[0][1], v[1][0], v[1][1]}, f32x4{v[2][0], v[2][1], v[3][0], v[3][1]}, h, m, l);
             const u32x4 pv[3] = {__builtin_bit_cast(u32x4, h), __builtin_bit_cast(u32x4, m), __builtin_bit_cast(u32x4, l)};
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                *reinterpret_cast<u32x2*>(base + ((2 * jp) * 3 + pl) * 2048) = u32x2{pv[pl][0], pv[pl][1]};
-                *reinterpret_cast<u32x2*>(base + ((2 * jp + 1) * 3 + pl) * 2048) = u32x2{pv[pl][2], pv[pl][3]};
-            }
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) *reinterpret_cast<unsigned*>(base + (j * 3 + pl) * PS) = pv[pl][j];
         }
     };
     // the 24 MFMAs of position (i, wj): U slot su x V slot sv, the 6 products of each of the
     // 4 blocks in wino_x6_kernel's order; the item's first chunk starts from C = 0
-    auto mma = [&](auto i_c, auto sl_c, auto first_c) {
+    auto mma = [&](auto i_c, auto su_c, auto sl_c, auto first_c) {
         constexpr int i = decltype(i_c)::value;
-        constexpr int sl = decltype(sl_c)::value;
+        constexpr int su = decltype(su_c)::value;     // U slot
+        constexpr int sl = decltype(sl_c)::value;     // V fragment slot
         constexpr bool FIRST = decltype(first_c)::value;
         if (PU_W4_ABL == 1) {
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb)
+            for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-                for (int tb = 0; tb < 2; ++tb)
-                    acc[i][cb][tb][0] += __builtin_bit_cast(float, __builtin_shufflevector(fu[sl][cb][0], fv[sl][tb][1], 0, 9));
+                for (int tb = 0; tb < NTB; ++tb)
+                    acc[i][cb][tb][0] += __builtin_bit_cast(float, __builtin_shufflevector(fu[su][cb][0], fv[sl][tb][1], 0, 9));
             return;
         }
         constexpr int PU[6] = {1, 2, 0, 1, 0, 0}, PV[6] = {1, 0, 2, 0, 1, 0};
 #pragma unroll
         for (int e = 0; e < 6; ++e)
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb)
+            for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-                for (int tb = 0; tb < 2; ++tb)
+                for (int tb = 0; tb < NTB; ++tb)
                     acc[i][cb][tb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                        fu[sl][cb][PU[e]], fv[sl][tb][PV[e]], (FIRST && e == 0) ? f32x16{} : acc[i][cb][tb], 0, 0, 0);
+                        fu[su][cb][PU[e]], fv[sl][tb][PV[e]], (FIRST && e == 0) ? f32x16{} : acc[i][cb][tb], 0, 0, 0);
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -726,8 +750,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // V ring: V(s) in slot s % 3 (byte offset sv), V(s+1) / V(s+2) in the next two
     unsigned sv = 0;
     auto slot_after = [](unsigned so, int k) -> unsigned {
-        unsigned r = so + (unsigned)k * W4_VH;
-        return r >= 3u * W4_VH ? r - 3u * W4_VH : r;
+        unsigned r = so + (unsigned)k * VS;
+        return r >= 3u * VS ? r - 3u * VS : r;
     };
 
     // sub-stage (kc, i) = s.  At barrier(s) every wave has finished s-1, so V(s+1) (formed during
@@ -742,24 +766,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // pin this sub-stage's fragments (U issued and V read during s-1) here: the MFMAs would
         // otherwise be hoisted across barrier(s) into sub-stage s-1
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
+        for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) asm volatile("" : "+v"(fu[i & 1][k][pl]), "+v"(fv[i & 1][k][pl]));
+            for (int k = 0; k < NCB; ++k) asm volatile("" : "+v"(fu[i & (USL - 1)][k][pl]));
+#pragma unroll
+            for (int k = 0; k < NTB; ++k) asm volatile("" : "+v"(fv[i & 1][k][pl]));
+        }
         // pin the window rows this formation reads (F = 2: rows 1, 2; 3: 1, 3; 0: 0, 2; 1: 1, 2):
         // the formation is pure VALU and would otherwise be hoisted across the barriers
         constexpr int RA = F == 0 ? 0 : 1, RB = F == 3 ? 3 : 2;
 #pragma unroll
         for (int ss = 0; ss < 4; ++ss) asm volatile("" : "+v"(d[RA * 4 + ss]), "+v"(d[RB * 4 + ss]));
         read_v(slot_after(sv, 1), std::integral_constant<int, (i + 1) & 1>{});
-        if constexpr (i < 3) load_u(kc, i + 1, std::integral_constant<int, (i + 1) & 1>{});
-        else load_u(kc + 1, 0, I0{});
-        mma(i_c, std::integral_constant<int, i & 1>{}, first_c);
+        if constexpr (i + UA < 4) load_u(kc, i + UA, std::integral_constant<int, (i + UA) & (USL - 1)>{});
+        else load_u(kc + 1, i + UA - 4, std::integral_constant<int, (i + UA) & (USL - 1)>{});
+        mma(i_c, std::integral_constant<int, i & (USL - 1)>{}, std::integral_constant<int, i & 1>{}, first_c);
         // pin this sub-stage's MFMAs here: they are pure, and the selection DAG of the unrolled
         // chunk would otherwise float them past the following barriers
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
+        for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-            for (int tb = 0; tb < 2; ++tb) asm volatile("" : "+a"(acc[i][cb][tb]));
+            for (int tb = 0; tb < NTB; ++tb) asm volatile("" : "+a"(acc[i][cb][tb]));
         make_v(std::integral_constant<int, F>{}, slot_after(sv, 2));
         if constexpr (i == 0) load_row(kc + 1, 2);
         if constexpr (i == 1) {
@@ -772,12 +799,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // issue order: V(s+1) fragment reads, U(s+1), then the 24 MFMAs with the formation of
         // V(s+2) in their shadow (~4 VALU per MFMA, a plane store every other one)
         // (the 12 plane stores are merged into 6 ds_write2st64 before scheduling)
-        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3 * NTB, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 3 * NCB, 0);     // U(s+UA)
 #pragma unroll
         for (int q = 0; q < 24; ++q) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, CPT == 4 ? 5 : 3, 0);
             if ((q & 3) == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
         }
         __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);
@@ -791,8 +818,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     load_row(kc0, 2);
     load_row(kc0, 3);
     load_u(kc0, 0, I0{});
+    if constexpr (UA == 2) load_u(kc0, 1, I1{});
     make_v(I0{}, 0u);
-    make_v(I1{}, (unsigned)W4_VH);
+    make_v(I1{}, (unsigned)VS);
     load_row(kc0 + 1, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -826,7 +854,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // the column received in round r in acc[0 / 1][block sent in round r]); Y in acc[3][py][px].
     auto xform = [&](auto j_c) {
         constexpr int J = decltype(j_c)::value;
-#define W4A(i, b) acc[i][(b) >> 1][(b) & 1]
+#define W4A(i, b) acc[i][(b) / NTB][(b) % NTB]
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             const float s0 = W4A(0, J)[e] + W4A(1, J)[e] + W4A(2, J)[e];
@@ -867,8 +895,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const float c0 = W4A(py, B0)[e], c1 = W4A(py, B1)[e], c2 = W4A(py, B2)[e], c3 = W4A(py, B3)[e];
-                acc[3][py][0][e] = (c0 + c1) + c2;      // Y[py][0] = (s0 + s1) + s2
-                acc[3][py][1][e] = c1 - (c2 + c3);      // Y[py][1] = s1 - (s2 + s3)
+                W4A(3, 2 * py)[e] = (c0 + c1) + c2;      // Y[py][0] = (s0 + s1) + s2
+                W4A(3, 2 * py + 1)[e] = c1 - (c2 + c3);  // Y[py][1] = s1 - (s2 + s3)
             }
 #undef W4A
     };
@@ -879,7 +907,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         default: xform(std::integral_constant<int, 3>{}); break;
     }
 
-    const int cbo = wj >> 1, tbo = wj & 1;
+    const int cbo = wj / NTB, tbo = wj % NTB;
     const int e_m = m_blk + 32 * tbo + (lane & 31), e_n = n_blk + 32 * cbo + 4 * (lane >> 5);
     const bool e_ok = e_m < w.tiles;
     const int em = e_ok ? e_m : 0;
@@ -889,12 +917,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int ty = t2 - b * (p.Ho >> 1);
     const long long pix00 = ((long long)b * p.Ho + 2 * ty) * p.Wo + 2 * tx;
     auto yv = [&](int py, int o, int g) {
-        return f32x4{acc[3][py][o][4 * g], acc[3][py][o][4 * g + 1], acc[3][py][o][4 * g + 2], acc[3][py][o][4 * g + 3]};
+        const int b2 = 2 * py + o;
+        const f32x16& a3 = acc[3][b2 / NTB][b2 % NTB];
+        return f32x4{a3[4 * g], a3[4 * g + 1], a3[4 * g + 2], a3[4 * g + 3]};
     };
     if (p.ksplit == 1) {
         // wino_x6_kernel's batched float4 epilogue for both output rows: operand loads first,
         // then the stores
-        const bool first = n_blk < p.n0;
+        const bool first = n_blk + 32 * cbo < p.n0;     // a 32-channel block lies in one destination
         const int ld = first ? p.n0 : p.N - p.n0;
         float* dst = first ? p.dst0 : p.dst1;
         const float* msk = first ? p.mask0 : p.mask1;
@@ -1511,8 +1541,13 @@ static bool wino128_on() {
     return on;
 }
 
+static bool wino4_on();
+static bool wino4_wide_on();
+// 32-tile x 128-channel items: the 8-wave wino128_x6_kernel (PU_WINO128=1 with PU_WINO4=0), or the
+// one-wave-per-SIMD kernel's wide items (PU_WINO4_WIDE=1)
 static bool wino128_use(const pu_conv_args* a) {
-    return wino128_on() && a->n % W2_BN == 0 && (a->n0 == a->n || a->n0 % 32 == 0);
+    const bool on = wino4_on() ? wino4_wide_on() : wino128_on();
+    return on && a->n % W2_BN == 0 && (a->n0 == a->n || a->n0 % 32 == 0);
 }
 
 bool wino_ok(const pu_conv_args* a, bool vec_epi) {
@@ -1575,6 +1610,16 @@ static bool wino4_on() {
     return on;
 }
 
+// the one-wave-per-SIMD kernel's 32-tile x 128-channel items (PU_WINO4_WIDE=1): bit-identical,
+// measured no faster than its 64 x 64 items (profiles/r06_experiments/wino4_ab.txt) - opt-in
+static bool wino4_wide_on() {
+    static const bool on = [] {
+        const char* e = getenv("PU_WINO4_WIDE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     WinoParams w;
     w.p = p;
@@ -1597,7 +1642,7 @@ int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     w.p.part = (float*)a->workspace;
     w.kc_per = per;
     const int items = w.gm * w.p.gn * ks;
-    if (w128) {
+    if (w128 && !wino4_on()) {
         if (wino_persist() && items > 256)
             hipLaunchKernelGGL(wino128_x6_kernel<true>, dim3(256), dim3(512), 0, s, w);
         else
@@ -1607,8 +1652,14 @@ int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {
     if (wino4_on()) {
         // one item per block (the pipelined kernel keeps the next chunks' rows in flight per item)
         const bool full = p.resid || p.cscale || (p.flags & PU_EPI_ACCUM);
-        if (full) hipLaunchKernelGGL(wino4_x6_kernel<true>, dim3((unsigned)items), dim3(256), 0, s, w);
-        else hipLaunchKernelGGL(wino4_x6_kernel<false>, dim3((unsigned)items), dim3(256), 0, s, w);
+        const dim3 g((unsigned)items);
+        if (w128) {
+            if (full) hipLaunchKernelGGL((wino4_x6_kernel<true, 4>), g, dim3(256), 0, s, w);
+            else hipLaunchKernelGGL((wino4_x6_kernel<false, 4>), g, dim3(256), 0, s, w);
+        } else {
+            if (full) hipLaunchKernelGGL((wino4_x6_kernel<true, 2>), g, dim3(256), 0, s, w);
+            else hipLaunchKernelGGL((wino4_x6_kernel<false, 2>), g, dim3(256), 0, s, w);
+        }
         return ks;
     }
     if (wino_persist() && items > 256)

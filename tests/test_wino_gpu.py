@@ -277,7 +277,7 @@ out = {}
 for (B, H, W, c0, c1, N) in [(2, 16, 16, 64, 0, 64), (3, 10, 14, 128, 0, 128), (2, 8, 8, 64, 64, 64),
                              (1, 32, 16, 128, 0, 192), (4, 8, 8, 512, 0, 512), (2, 16, 16, 256, 256, 256),
                              (1, 2, 2, 32, 0, 64), (5, 128, 128, 64, 0, 64), (3, 96, 80, 128, 0, 192),
-                             (2, 24, 24, 128, 128, 128)]:
+                             (2, 24, 24, 128, 128, 128), (2, 24, 24, 64, 64, 64), (3, 16, 16, 64, 0, 128)]:
     g = torch.Generator().manual_seed(B + H + W + c0 + c1 + N)
     C = c0 + c1
     x = torch.randn(B, H, W, C, generator=g).relu().cuda()
@@ -307,8 +307,9 @@ torch.save(out, sys.argv[1])
 
 
 def test_wino4_bit_identical_to_8_wave_kernel(tmp_path):
-    """wino4_x6_kernel (one wave per SIMD, 2 x 2 MFMA blocks per position, U from L2 into
-    registers) and wino_x6_kernel (PU_WINO4=0; read once per process - two child processes) form
+    """wino4_x6_kernel (one wave per SIMD, 2 x 2 or 4 x 1 MFMA blocks per position - 64 x 64 or, for
+    n % 128 == 0, 32-tile x 128-channel items -, U from L2 into registers) and wino_x6_kernel
+    (PU_WINO4=0; read once per process - two child processes) form
     every accumulator from the same U / V planes in the same product order and run the same
     output-transform expression tree: forward, data gradient (masks, concat split), residual and
     accumulate epilogues bitwise equal - one and many items per block, split-K, concat sources,
@@ -318,15 +319,16 @@ def test_wino4_bit_identical_to_8_wave_kernel(tmp_path):
     import sys
     root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plastic-unet_amd")
     res = {}
-    for on in ("1", "0"):
+    for on in ("10", "11", "00"):       # (PU_WINO4, PU_WINO4_WIDE)
         f = str(tmp_path / ("w%s.pt" % on))
-        env = dict(os.environ, PU_WINO4=on, PU_WINO="1")
+        env = dict(os.environ, PU_WINO4=on[0], PU_WINO4_WIDE=on[1], PU_WINO="1")
         r = subprocess.run([sys.executable, "-c", _W4_SCRIPT, f, root], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         res[on] = torch.load(f, weights_only=True)
-    for k in res["1"]:
-        for i, (a, b) in enumerate(zip(res["1"][k], res["0"][k])):
-            assert (a is None) == (b is None), k
-            if a is not None:
-                assert torch.equal(a, b), (k, i, (a - b).abs().max().item())
+    for v in ("10", "11"):
+        for k in res[v]:
+            for i, (a, b) in enumerate(zip(res[v][k], res["00"][k])):
+                assert (a is None) == (b is None), k
+                if a is not None:
+                    assert torch.equal(a, b), (v, k, i, (a - b).abs().max().item())
