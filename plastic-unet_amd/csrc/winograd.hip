@@ -554,7 +554,10 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 //     both output rows and runs the batched float4 epilogue.
 #ifndef PU_W4_ABL
 #define PU_W4_ABL 0     // ablations (timing only, wrong results): 1 no MFMAs, 2 no V formation,
-                        // 4 no window loads, 5 no U loads
+                        // 4 no window loads, 5 no U loads, 6 no sub-stage barrier, 7 no V plane stores
+#endif
+#ifndef PU_W4_VA
+#define PU_W4_VA 2      // V formed PU_W4_VA sub-stages ahead into a (PU_W4_VA + 1)-slot ring (2 or 3)
 #endif
 constexpr int W4_VH = 4 * 3 * 64 * 32;         // 24 KB: V of one sub-stage (4 xi x 3 planes x 64 tiles x 16)
 constexpr int W4_XF = 4 * 2 * 16 * 64;         // floats in one exchange round (32 KB, inside the V ring)
@@ -573,7 +576,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // U fragments UA sub-stages ahead in a USL-slot register ring (2 ahead for 64-channel items;
     // the 128-channel items' 12 fragments per sub-stage only fit one ahead)
     constexpr int UA = NCB == 2 ? 2 : 1, USL = 2 * UA;
-    __shared__ __attribute__((aligned(16))) unsigned char ldv[3 * W4_VH];
+    constexpr int VA = PU_W4_VA, NVS = VA + 1;
+    static_assert(VA == 2 || VA == 3, "V lead");
+    __shared__ __attribute__((aligned(16))) unsigned char ldv[NVS * W4_VH];
     float* const xch = reinterpret_cast<float*>(ldv);
 
     const int tid = threadIdx.x;
@@ -705,6 +710,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 const u32x4 pv[3] = {__builtin_bit_cast(u32x4, h), __builtin_bit_cast(u32x4, m), __builtin_bit_cast(u32x4, l)};
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) {
+                    if (PU_W4_ABL == 7) {      // formation without its plane stores (timing only)
+                        asm volatile("" :: "v"(pv[pl]));
+                        continue;
+                    }
                     *reinterpret_cast<u32x2*>(base + ((2 * jp) * 3 + pl) * PS) = u32x2{pv[pl][0], pv[pl][1]};
                     *reinterpret_cast<u32x2*>(base + ((2 * jp + 1) * 3 + pl) * PS) = u32x2{pv[pl][2], pv[pl][3]};
                 }
@@ -747,11 +756,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
 
-    // V ring: V(s) in slot s % 3 (byte offset sv), V(s+1) / V(s+2) in the next two
+    // V ring: V(s) in slot s % NVS (byte offset sv), V(s+1) .. V(s+VA) in the next VA
     unsigned sv = 0;
     auto slot_after = [](unsigned so, int k) -> unsigned {
         unsigned r = so + (unsigned)k * VS;
-        return r >= 3u * VS ? r - 3u * VS : r;
+        return r >= (unsigned)(NVS * VS) ? r - (unsigned)(NVS * VS) : r;
     };
 
     // sub-stage (kc, i) = s.  At barrier(s) every wave has finished s-1, so V(s+1) (formed during
@@ -759,9 +768,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // V(s+2).  The MFMAs use the V fragments read during s-1 and the U fragments issued during s-1.
     auto sub = [&](int kc, auto i_c, auto first_c) {
         constexpr int i = decltype(i_c)::value;
-        constexpr int F = (i + 2) & 3;                 // the row formed now (chunk kc, or kc+1 for i >= 2)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        constexpr int F = (i + VA) & 3;                // the row formed now (chunk kc, or kc+1 for i >= 4 - VA)
+        if (PU_W4_ABL != 6) {
+            // VA = 3: V(s+1) was stored during s-2, older than every LDS op of s-1 (3 NTB
+            // fragment reads, then >= 3 NTB plane stores); LDS ops complete in order, so <= 3 NTB
+            // outstanding means only s-1's youngest stores are in flight across the barrier
+            if constexpr (VA == 3) asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(3 * NTB) : "memory");
+            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
         asm volatile("" ::: "memory");
         // pin this sub-stage's fragments (U issued and V read during s-1) here: the MFMAs would
         // otherwise be hoisted across barrier(s) into sub-stage s-1
@@ -787,13 +802,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
             for (int tb = 0; tb < NTB; ++tb) asm volatile("" : "+a"(acc[i][cb][tb]));
-        make_v(std::integral_constant<int, F>{}, slot_after(sv, 2));
-        if constexpr (i == 0) load_row(kc + 1, 2);
-        if constexpr (i == 1) {
-            load_row(kc + 1, 1);
-            load_row(kc + 1, 3);
+        make_v(std::integral_constant<int, F>{}, slot_after(sv, VA));
+        if constexpr (VA == 2) {
+            if constexpr (i == 0) load_row(kc + 1, 2);
+            if constexpr (i == 1) {
+                load_row(kc + 1, 1);
+                load_row(kc + 1, 3);
+            }
+            if constexpr (i == 2) load_row(kc + 2, 0);
+        } else {
+            // rows 1 / 3 of chunk kc are dead after row 3's formation (i = 0), row 0 of kc+1
+            // after its row 0 (i = 1), row 2 of kc+1 after its row 2 (i = 3)
+            if constexpr (i == 0) {
+                load_row(kc + 1, 1);
+                load_row(kc + 1, 3);
+            }
+            if constexpr (i == 1) load_row(kc + 2, 0);
+            if constexpr (i == 3) load_row(kc + 2, 2);
         }
-        if constexpr (i == 2) load_row(kc + 2, 0);
         sv = slot_after(sv, 1);
 #if PU_W4_ABL == 0 && !PU_NO_ILV
         // issue order: V(s+1) fragment reads, U(s+1), then the 24 MFMAs with the formation of
@@ -821,7 +847,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if constexpr (UA == 2) load_u(kc0, 1, I1{});
     make_v(I0{}, 0u);
     make_v(I1{}, (unsigned)VS);
+    if constexpr (VA == 3) make_v(std::integral_constant<int, 2>{}, (unsigned)(2 * VS));
     load_row(kc0 + 1, 0);
+    if constexpr (VA == 3) load_row(kc0 + 1, 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
