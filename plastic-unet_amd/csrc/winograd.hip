@@ -1570,11 +1570,13 @@ static bool wino128_on() {
 }
 
 static bool wino4_on();
-static bool wino4_wide_on();
 // 32-tile x 128-channel items: the 8-wave wino128_x6_kernel (PU_WINO128=1 with PU_WINO4=0), or the
 // one-wave-per-SIMD kernel's wide items (PU_WINO4_WIDE=1)
+static int wino4_wide_mode();
 static bool wino128_use(const pu_conv_args* a) {
-    const bool on = wino4_on() ? wino4_wide_on() : wino128_on();
+    const int C = a->c0 + a->c1;
+    const int wm = wino4_wide_mode();
+    const bool on = wino4_on() ? (wm == 1 || (wm == 2 && C < 128 && a->n > WG_BN)) : wino128_on();
     return on && a->n % W2_BN == 0 && (a->n0 == a->n || a->n0 % 32 == 0);
 }
 
@@ -1638,14 +1640,17 @@ static bool wino4_on() {
     return on;
 }
 
-// the one-wave-per-SIMD kernel's 32-tile x 128-channel items (PU_WINO4_WIDE=1): bit-identical,
-// measured no faster than its 64 x 64 items (profiles/r06_experiments/wino4_ab.txt) - opt-in
-static bool wino4_wide_on() {
-    static const bool on = [] {
+// the one-wave-per-SIMD kernel's 32-tile x 128-channel items: PU_WINO4_WIDE=1 for every layer with
+// n % 128 == 0 (bit-identical, measured no faster than the 64 x 64 items,
+// profiles/r06_experiments/wino4_ab.txt); =2 (default) only for the short reductions (C < 128)
+// into several 64-channel blocks, which the 64 x 64 items leave to the direct kernel (the concat
+// data gradients: top 0.426 -> 0.409 ms, l2 0.200 -> 0.195); =0 none
+static int wino4_wide_mode() {
+    static const int m = [] {
         const char* e = getenv("PU_WINO4_WIDE");
-        return e && e[0] == '1';
+        return !e ? 2 : e[0] == '1' ? 1 : e[0] == '2' ? 2 : 0;
     }();
-    return on;
+    return m;
 }
 
 int wino_launch(const pu_conv_args* a, IgemmParams p, hipStream_t s) {

@@ -83,8 +83,12 @@ def set_wino(on):
     return prev
 
 
-# the library's PU_WINO128 switch (csrc/winograd.hip reads the same variable once per process)
-_WINO128 = os.environ.get("PU_WINO128", "0") == "1"
+# 32-tile x 128-channel Winograd items (csrc/winograd.hip wino128_use reads the same variables once
+# per process): the one-wave-per-SIMD kernel's wide items (PU_WINO4_WIDE=1 everywhere, =2 - the
+# default - for the short reductions only, =0 none), or with PU_WINO4=0 the 8-wave PU_WINO128=1 kernel
+_WINO4 = os.environ.get("PU_WINO4", "1") != "0"
+_WINO128 = os.environ.get("PU_WINO4_WIDE", "2") in ("1", "2") if _WINO4 else \
+    os.environ.get("PU_WINO128", "0") == "1"
 
 
 def wino_wanted(w, mode):

@@ -257,7 +257,7 @@ def test_wino128_bit_identical_to_64_channel_items(tmp_path):
     res = {}
     for on in ("1", "0"):
         f = str(tmp_path / ("w%s.pt" % on))
-        env = dict(os.environ, PU_WINO128=on, PU_WINO="1")
+        env = dict(os.environ, PU_WINO4="0", PU_WINO128=on, PU_WINO="1")
         r = subprocess.run([sys.executable, "-c", _W128_SCRIPT, f, root], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
@@ -319,16 +319,18 @@ def test_wino4_bit_identical_to_8_wave_kernel(tmp_path):
     import sys
     root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plastic-unet_amd")
     res = {}
-    for on in ("10", "11", "00"):       # (PU_WINO4, PU_WINO4_WIDE)
+    # (PU_WINO4, PU_WINO4_WIDE, PU_WINO128): the short-reduction concat data gradients take the
+    # direct kernel in "100" / "000" and 128-channel Winograd items in the others
+    for on in ("100", "000", "110", "120", "001"):
         f = str(tmp_path / ("w%s.pt" % on))
-        env = dict(os.environ, PU_WINO4=on[0], PU_WINO4_WIDE=on[1], PU_WINO="1")
+        env = dict(os.environ, PU_WINO4=on[0], PU_WINO4_WIDE=on[1], PU_WINO128=on[2], PU_WINO="1")
         r = subprocess.run([sys.executable, "-c", _W4_SCRIPT, f, root], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         res[on] = torch.load(f, weights_only=True)
-    for v in ("10", "11"):
+    for v, ref in (("100", "000"), ("110", "001"), ("120", "001")):
         for k in res[v]:
-            for i, (a, b) in enumerate(zip(res[v][k], res["00"][k])):
+            for i, (a, b) in enumerate(zip(res[v][k], res[ref][k])):
                 assert (a is None) == (b is None), k
                 if a is not None:
                     assert torch.equal(a, b), (v, k, i, (a - b).abs().max().item())
