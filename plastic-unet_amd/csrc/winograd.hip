@@ -559,6 +559,20 @@ __global__ __launch_bounds__(512) void wino_x6_kernel(const WinoParams w) {
 #ifndef PU_W4_VA
 #define PU_W4_VA 2      // V formed PU_W4_VA sub-stages ahead into a (PU_W4_VA + 1)-slot ring (2 or 3)
 #endif
+#ifndef PU_W4_ITEM_STAMP
+#define PU_W4_ITEM_STAMP 0  // diagnostic build: per-block s_memtime at entry / prologue / loop end / exchange / exit
+#endif
+#if PU_W4_ITEM_STAMP
+constexpr int PU_W4_NBLK = 4096;
+__device__ unsigned long long pu_w4_item_buf[PU_W4_NBLK * 8];
+// lane 0 of wave 0, blocks < PU_W4_NBLK: stamp k (vector stores; timing only, tools/w4_items.py)
+__device__ __forceinline__ void w4_item_stamp(int k, unsigned long long v) {
+    if (threadIdx.x == 0 && blockIdx.x < PU_W4_NBLK) pu_w4_item_buf[blockIdx.x * 8 + k] = v;
+}
+#define W4S(k) w4_item_stamp(k, __builtin_amdgcn_s_memtime())
+#else
+#define W4S(k) ((void)0)
+#endif
 constexpr int W4_VH = 4 * 3 * 64 * 32;         // 24 KB: V of one sub-stage (4 xi x 3 planes x 64 tiles x 16)
 constexpr int W4_XF = 4 * 2 * 16 * 64;         // floats in one exchange round (32 KB, inside the V ring)
 
@@ -584,6 +598,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);   // position column j of this wave
+    W4S(0);
+#if PU_W4_ITEM_STAMP
+    w4_item_stamp(6, (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)));    // HW_ID
+    w4_item_stamp(7, (unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)));   // XCC_ID
+#endif
 
     // ---- the item (one per block, XCD-aware order)
     const int item = xcd_remap(blockIdx.x, gridDim.x);
@@ -854,6 +873,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     read_v(0u, I0{});
+    W4S(1);
 
     using BT = std::true_type;
     using BF = std::false_type;
@@ -873,6 +893,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    W4S(2);
 
     // ---- output transform.  Column sums s_py[j] (lane-local, wino_x6_kernel's order):
     // s_0 = (M0 + M1) + M2, s_1 = (M1 - M2) - M3.  Wave b owns block b = (cb, tb) = (b >> 1,
@@ -935,6 +956,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         default: xform(std::integral_constant<int, 3>{}); break;
     }
 
+    W4S(3);
     const int cbo = wj / NTB, tbo = wj % NTB;
     const int e_m = m_blk + 32 * tbo + (lane & 31), e_n = n_blk + 32 * cbo + 4 * (lane >> 5);
     const bool e_ok = e_m < w.tiles;
@@ -1058,7 +1080,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 for (int g = 0; g < 4; ++g)
                     *reinterpret_cast<f32x4*>(part + ((long long)py * p.Wo + o) * p.N + 8 * g) = yv(py, o, g);
     }
+    W4S(4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    W4S(5);
 }
 
 // ------------------------------------------------------------------ 128-channel Winograd items
@@ -1719,6 +1743,16 @@ using namespace pu;
 extern "C" int pu_wpp_stamps(unsigned long long* dst, int n) {
     if (n > 8 * PU_WPP_NSTAMP) n = 8 * PU_WPP_NSTAMP;
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(pu_wpp_stamp_buf), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? n : -1;
+}
+#endif
+
+#if PU_W4_ITEM_STAMP
+// diagnostic build only: per-block item stamps of the last wino4 launch ([block][8]: entry,
+// prologue done, loop done, exchange done, stores issued, stores drained, HW_ID, XCC_ID)
+extern "C" int pu_w4_item_stamps(unsigned long long* dst, int n) {
+    if (n > 8 * PU_W4_NBLK) n = 8 * PU_W4_NBLK;
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(pu_w4_item_buf), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
                ? n : -1;
 }
 #endif
