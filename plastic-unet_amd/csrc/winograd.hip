@@ -575,6 +575,11 @@ __device__ __forceinline__ void w4_item_stamp(int k, unsigned long long v) {
 #endif
 constexpr int W4_VH = 4 * 3 * 64 * 32;         // 24 KB: V of one sub-stage (4 xi x 3 planes x 64 tiles x 16)
 constexpr int W4_XF = 4 * 2 * 16 * 64;         // floats in one exchange round (32 KB, inside the V ring)
+#ifndef PU_W4_XCH1
+#define PU_W4_XCH1 1    // 1: the output exchange in one round (96 KB: every wave's 3 outbound blocks at
+                        // once, 16-byte LDS accesses, one barrier); 0: 3 rounds through the V ring
+#endif
+constexpr int W4_X1 = 4 * 3 * 32 * 64;         // floats of the one-round exchange (4 waves x 3 blocks)
 
 template <bool FULL, int NCB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wino4_x6_kernel(const WinoParams w) {
@@ -592,7 +597,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr int UA = NCB == 2 ? 2 : 1, USL = 2 * UA;
     constexpr int VA = PU_W4_VA, NVS = VA + 1;
     static_assert(VA == 2 || VA == 3, "V lead");
-    __shared__ __attribute__((aligned(16))) unsigned char ldv[NVS * W4_VH];
+    // one-round exchange except in the wide items' general epilogue (its operands leave no room)
+    constexpr bool XCH1 = PU_W4_XCH1 && !(FULL && NCB == 4);
+    constexpr int LDV = XCH1 && W4_X1 * 4 > NVS * W4_VH ? W4_X1 * 4 : NVS * W4_VH;
+    __shared__ __attribute__((aligned(16))) unsigned char ldv[LDV];
     float* const xch = reinterpret_cast<float*>(ldv);
 
     const int tid = threadIdx.x;
@@ -911,6 +919,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             W4A(0, J)[e] = s0;
             W4A(1, J)[e] = s1;
         }
+        if constexpr (XCH1) {
+        // region (source wave w, round r) = 8 float4 chunks x 64 lanes: the 32 column sums of the
+        // block wave w sends in round r (s_0[16], s_1[16]); chunk c holds values 4c .. 4c+3
+        auto region = [&](int wsrc, int r) { return reinterpret_cast<f32x4*>(xch) + (wsrc * 3 + r - 1) * 8 * 64; };
+        auto send = [&](auto r_c) {
+            constexpr int R = decltype(r_c)::value;
+            constexpr int SB = (J + R) & 3;
+            f32x4* dst = region(J, R);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                f32x4 v;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int e = (4 * c + q) & 15;
+                    v[q] = c < 4 ? W4A(0, SB)[e] + W4A(1, SB)[e] + W4A(2, SB)[e]
+                                 : W4A(1, SB)[e] - W4A(2, SB)[e] - W4A(3, SB)[e];
+                }
+                dst[c * 64 + lane] = v;
+                if (c == 3) asm volatile("" ::: "memory");
+            }
+        };
+        auto recv = [&](auto r_c) {
+            constexpr int R = decltype(r_c)::value;
+            constexpr int SB = (J + R) & 3, FROM = (J - R) & 3;
+            const f32x4* src = region(FROM, R);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const f32x4 v = src[c * 64 + lane];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int e = (4 * c + q) & 15;
+                    if (c < 4) W4A(0, SB)[e] = v[q];
+                    else W4A(1, SB)[e] = v[q];
+                }
+                if (c == 3) asm volatile("" ::: "memory");
+            }
+        };
+        // (compiler fences between the blocks: one block's 32 values in registers at a time)
+        send(std::integral_constant<int, 1>{});
+        asm volatile("" ::: "memory");
+        send(std::integral_constant<int, 2>{});
+        asm volatile("" ::: "memory");
+        send(std::integral_constant<int, 3>{});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        recv(std::integral_constant<int, 1>{});
+        asm volatile("" ::: "memory");
+        recv(std::integral_constant<int, 2>{});
+        asm volatile("" ::: "memory");
+        recv(std::integral_constant<int, 3>{});
+        } else {
         float* xs = xch + J * (2 * 16 * 64);
         auto round = [&](auto r_c) {
             constexpr int R = decltype(r_c)::value;
@@ -936,6 +996,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         round(std::integral_constant<int, 1>{});
         round(std::integral_constant<int, 2>{});
         round(std::integral_constant<int, 3>{});
+        }
         // column j was received in round r = (J - j) & 3 and sits in block (J + r) & 3 (r = 0: own)
         constexpr int B0 = (J + ((J - 0) & 3)) & 3, B1 = (J + ((J - 1) & 3)) & 3;
         constexpr int B2 = (J + ((J - 2) & 3)) & 3, B3 = (J + ((J - 3) & 3)) & 3;
