@@ -1161,6 +1161,351 @@ __global__ __launch_bounds__(512) void wgrad_wino_x6_kernel(const WinoWgradParam
     }
 }
 
+// ------------------------------------ Winograd-domain weight gradient on one wave per SIMD
+// wgrad_wino_x6_kernel's arithmetic (the same Dhat / Ehat planes, the same 6 products per
+// accumulator in the same order over the same 16-tile k-steps, the same G^T M G expression tree)
+// on 4 waves with 256 accumulator registers each: wave wj owns position column j = wj (the 4
+// positions (i, wj)) and all 2 x 2 32-channel blocks (input block cb x output block nb) of the
+// block's 64 x 64 channels, so every X fragment feeds 2 MFMAs and every G fragment 2 - 12 fragment
+// reads per 24 MFMAs instead of 12 per 12 (the 8-wave kernel moves 96 KB of LDS reads per
+// sub-stage for 48 KB of plane stores; here 48 KB).  Producer role: thread (tile pt, channel quad
+// cq) forms 4 channels with 16-byte window loads and 8-byte plane stores (the 8-wave kernel's two
+// neighbouring channel-pair threads, the same bytes).  Output transform: wave wj forms
+// R[r][j] = sum_a G[a][r] M[a][j] for all 4 blocks; per r one exchange round gives wave b all four
+// R[r][j] of block b = (cb, nb) = (b >> 1, b & 1), which then forms dW[r][s] = P0 + P1 exactly as
+// the 8-wave kernel's wave pairs do.  Bit-identical to wgrad_wino_x6_kernel.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgrad_wino4_x6_kernel(const WinoWgradParams w) {
+#pragma clang fp contract(off)
+    const WgradParams& p = w.p;
+    __shared__ __attribute__((aligned(16))) char lx0[WW_SLOT];
+    __shared__ __attribute__((aligned(16))) char lx1[WW_SLOT];
+    __shared__ __attribute__((aligned(16))) char lg0[WW_SLOT];
+    __shared__ __attribute__((aligned(16))) char lg1[WW_SLOT];
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wj = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int cx = blk % p.gx;
+    const int rest = blk / p.gx;
+    const int ny = rest % p.gy;
+    const int z = rest / p.gy;
+    const int t_begin = z * w.tps;
+    const int t_end = min(w.tiles, t_begin + w.tps);
+    const int S = (t_end - t_begin + 15) >> 4;
+
+    // ---- producer role: tile pt of a stage, channel quad cq of the 64 input / 64 output channels
+    const int pt = tid >> 4, cq = tid & 15;
+    const int c_lo = cx * 64;
+    const bool first = c_lo < p.c0;
+    const int cs = first ? p.c0 : p.c1;
+    const int shift = p.Wi + 1;
+    const __amdgpu_buffer_rsrc_t xr = ww_rsrc((first ? p.src0 : p.src1) - (long long)shift * cs,
+                                              first ? w.x0_bytes : w.x1_bytes);
+    const __amdgpu_buffer_rsrc_t gr = ww_rsrc(p.P, w.p_bytes);
+    const unsigned pixb = (unsigned)cs * 4u;
+    const unsigned xco = (unsigned)((first ? c_lo : c_lo - p.c0) + 4 * cq) * 4u;
+    const unsigned gco = (unsigned)(ny * 64 + 4 * cq) * 4u;
+    const unsigned gpix = (unsigned)p.N * 4u;
+    const int st_off = hx_off(pt, 4 * cq);    // the thread's 8-byte slot in every image
+
+    unsigned xv[4];
+    bool xc0 = false, xc3 = false;
+    auto decode_x = [&](int k) {
+        const int m = t_begin + 16 * k + pt;
+        const bool mv = m < t_end;
+        int ty = 0, tx = 0, b = 0;
+        if (mv) {
+            const int t2 = fdiv(m, w.dTw);
+            tx = m - t2 * (p.Wo >> 1);
+            b = fdiv(t2, w.dTh);
+            ty = t2 - b * (p.Ho >> 1);
+        }
+        const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+        const unsigned base = (unsigned)(((b * p.Hi + y0) * p.Wi + x0 + shift) * cs) * 4u + xco;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            xv[r] = mv && (unsigned)(y0 + r) < (unsigned)p.Hi ? base + (unsigned)(r * p.Wi) * pixb : LEAN_OOB;
+        xc0 = x0 >= 0;
+        xc3 = x0 + 3 < p.Wi;
+    };
+    unsigned gv[2];
+    auto decode_g = [&](int k) {
+        const int m = t_begin + 16 * k + pt;
+        if (m < t_end) {
+            const int t2 = fdiv(m, w.dTw);
+            const int tx = m - t2 * (p.Wo >> 1);
+            const int b = fdiv(t2, w.dTh);
+            const int ty = t2 - b * (p.Ho >> 1);
+            const unsigned base = (unsigned)((b * p.Ho + 2 * ty) * p.Wo + 2 * tx) * gpix + gco;
+            gv[0] = base;
+            gv[1] = base + (unsigned)p.Wo * gpix;
+        } else {
+            gv[0] = gv[1] = LEAN_OOB;
+        }
+    };
+    f32x4 d[4][4], e[2][2];
+    auto load_x = [&](int r) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            unsigned vo = xv[r];
+            if (s == 0) vo = xc0 ? vo : LEAN_OOB;
+            if (s == 3) vo = xc3 ? vo : LEAN_OOB;
+            d[r][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    xr, vo, __builtin_amdgcn_readfirstlane(s * pixb), 0));
+        }
+    };
+    auto load_g = [&](int a) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            e[a][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    gr, gv[a], __builtin_amdgcn_readfirstlane(s * gpix), 0));
+    };
+    // 4 fp32 values -> their hi / mid / lo bf16 planes at b (+ WW_IMG, + 2 WW_IMG), two pairs
+    auto put = [&](char* b, const f32x4 v) {
+        unsigned h0, m0, l0, h1, m1, l1;
+        ww_split(wg_f32x2{v[0], v[1]}, h0, m0, l0);
+        ww_split(wg_f32x2{v[2], v[3]}, h1, m1, l1);
+        *reinterpret_cast<u32x2*>(b) = u32x2{h0, h1};
+        *reinterpret_cast<u32x2*>(b + WW_IMG) = u32x2{m0, m1};
+        *reinterpret_cast<u32x2*>(b + 2 * WW_IMG) = u32x2{l0, l1};
+    };
+    // row i of Dhat and Ehat for this thread's 4 channels (wgrad_wino_x6_kernel's expressions)
+    auto form = [&](auto i_c, char* sx, char* sg) {
+        constexpr int i = decltype(i_c)::value;
+        f32x4 t[4], u[2];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if constexpr (i == 0) t[s] = d[0][s] - d[2][s];
+            else if constexpr (i == 1) t[s] = d[1][s] + d[2][s];
+            else if constexpr (i == 2) t[s] = d[2][s] - d[1][s];
+            else t[s] = d[1][s] - d[3][s];
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            if constexpr (i == 0) u[s] = e[0][s];
+            else if constexpr (i == 1) u[s] = e[0][s] + e[1][s];
+            else if constexpr (i == 2) u[s] = e[0][s] - e[1][s];
+            else u[s] = e[1][s];
+        }
+        const f32x4 dv[4] = {t[0] - t[2], t[1] + t[2], t[2] - t[1], t[1] - t[3]};
+        const f32x4 ev[4] = {u[0], u[0] + u[1], u[0] - u[1], u[1]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            put(sx + 3 * j * WW_IMG + st_off, dv[j]);
+            put(sg + 3 * j * WW_IMG + st_off, ev[j]);
+        }
+    };
+
+    // ---- MFMA role: transposed fragment reads of position (i, wj), blocks cb / nb
+    const int grp = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
+    const int rsub = 8 * (grp >> 1) + gq;
+    const int ccol = 16 * (grp & 1) + 4 * gp;
+    const int xa0 = hx_off(rsub, ccol) + 3 * wj * WW_IMG;
+    const int xa1 = hx_off(rsub, 32 + ccol) + 3 * wj * WW_IMG;
+    auto tr2 = [&](const char* a) {
+        const wi16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)a);
+        const wi16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)(a + 4 * 128));
+        typedef short wi16x8 __attribute__((ext_vector_type(8)));
+        const wi16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        return __builtin_bit_cast(wg_bf16x8, av);
+    };
+    f32x16 acc[4][2][2];                      // [i][cb][nb]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][a][b][r] = 0.f;
+    auto mma = [&](auto i_c, const char* sx, const char* sg) {
+        constexpr int i = decltype(i_c)::value;
+        wg_bf16x8 q[2][3], g[2][3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+            q[0][pl] = tr2(sx + xa0 + pl * WW_IMG);
+            q[1][pl] = tr2(sx + xa1 + pl * WW_IMG);
+            g[0][pl] = tr2(sg + xa0 + pl * WW_IMG);
+            g[1][pl] = tr2(sg + xa1 + pl * WW_IMG);
+        }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                f32x16 c = acc[i][cb][nb];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[cb][1], g[nb][1], c, 0, 0, 0);   // small terms first
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[cb][2], g[nb][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[cb][0], g[nb][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[cb][1], g[nb][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[cb][0], g[nb][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q[cb][0], g[nb][0], c, 0, 0, 0);
+                acc[i][cb][nb] = c;
+            }
+    };
+    f32x4 bsum = {0.f, 0.f, 0.f, 0.f};        // dbias partial of the thread's 4 output channels
+
+    // sub-stage (k, i): the MFMAs of row i from slot i & 1, row i + 1 (or the next stage's row 0)
+    // formed into the other slot, then the reloads of wgrad_wino_x6_kernel's schedule
+    auto sub = [&](int k, auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        char* sx = (i & 1) ? lx1 : lx0;
+        char* sg = (i & 1) ? lg1 : lg0;
+        char* nx = (i & 1) ? lx0 : lx1;
+        char* ng = (i & 1) ? lg0 : lg1;
+        mma(i_c, sx, sg);
+        form(std::integral_constant<int, (i + 1) & 3>{}, nx, ng);
+        if constexpr (i == 1) {               // d row 2 and e row 0 are dead: next stage's
+            load_x(2);
+            bsum += e[0][0] + e[0][1];
+            decode_g(k + 1);
+            load_g(0);
+        } else if constexpr (i == 2) {        // d rows 1, 3 and e row 1 are dead
+            load_x(1);
+            load_x(3);
+            bsum += e[1][0] + e[1][1];
+            load_g(1);
+        } else if constexpr (i == 3) {        // d row 0 of stage k + 1 was used: stage k + 2's
+            decode_x(k + 2);
+            load_x(0);
+        }
+#if !PU_NO_ILV
+        // fragment reads first, then the 24 MFMAs with the formation (~6 VALU and one 8-byte plane
+        // store per MFMA) in their shadow
+        __builtin_amdgcn_sched_group_barrier(0x100, 24, 0);
+#pragma unroll
+        for (int q = 0; q < 24; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+#endif
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    decode_x(0);
+    load_x(0);
+    load_x(1);
+    load_x(2);
+    load_x(3);
+    decode_g(0);
+    load_g(0);
+    load_g(1);
+    form(std::integral_constant<int, 0>{}, lx0, lg0);
+    decode_x(1);
+    load_x(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int k = 0; k < S; ++k) {
+        sub(k, std::integral_constant<int, 0>{});
+        sub(k, std::integral_constant<int, 1>{});
+        sub(k, std::integral_constant<int, 2>{});
+        sub(k, std::integral_constant<int, 3>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+    float* slab = p.slab + (long long)z * p.Nr * p.Kcp;
+    // ---- bias: column sums of dZ over the split, fixed order (thread stages, then the 16 tiles)
+    if (p.bias_mode == 1 && cx == 0) {
+        f32x4* red = reinterpret_cast<f32x4*>(lg0);
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < 16) {
+            f32x4 v = red[tid];
+            for (int r = 1; r < 16; ++r) v += red[r * 16 + tid];
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) slab[(long long)(ny * 64 + 4 * tid + e4) * p.Kcp + p.K] = v[e4];
+        }
+        __syncthreads();
+    }
+
+    // ---- output transform dW = G^T M G, round r: R[r][j] of all 4 blocks on wave j, blocks
+    // exchanged (region (source wave, its round-slot) = 16 floats x 64 lanes, 6 regions in lx0 and
+    // 6 in lg0), then wave b forms dW[r][s] = P0 + P1 of block b.  Signs: M = s_i s_j M'.
+    const int cbo = wj >> 1, nbo = wj & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int n = ny * 64 + nbo * 32 + lr;
+    auto region = [&](int src, int slot) -> float* {
+        const int rg = src * 3 + slot;
+        return reinterpret_cast<float*>(rg < 6 ? lx0 : lg0) + (rg % 6) * 16 * 64;
+    };
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        float Rm[2][2][16];                   // this wave's R[r][wj] of every block
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                for (int idx = 0; idx < 16; ++idx) {
+                    const float m0 = acc[0][cb][nb][idx], m1 = acc[1][cb][nb][idx];
+                    const float m2 = acc[2][cb][nb][idx], m3 = -acc[3][cb][nb][idx];
+                    const float v = r == 0 ? m0 + 0.5f * (m1 + m2) : r == 1 ? 0.5f * (m1 - m2) : 0.5f * (m1 + m2) + m3;
+                    Rm[cb][nb][idx] = wj == 3 ? -v : v;
+                }
+        // send the 3 other blocks' values: block b goes to slot (b - wj - 1) & 3 ... (3 slots)
+#pragma unroll
+        for (int bo = 1; bo < 4; ++bo) {
+            const int b = (wj + bo) & 3;
+            float* dst = region(wj, bo - 1);
+#pragma unroll
+            for (int idx = 0; idx < 16; ++idx) {
+                float v = 0.f;
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb)
+                    if (bb == b) v = Rm[bb >> 1][bb & 1][idx];
+                dst[idx * 64 + lane] = v;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // R[r][j] of block wj for j = 0..3 (own: Rm; from wave j: its slot (wj - j - 1) & 3)
+        float Rj[4][16];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j == wj) {
+#pragma unroll
+                for (int idx = 0; idx < 16; ++idx) {
+                    float v = 0.f;
+#pragma unroll
+                    for (int bb = 0; bb < 4; ++bb)
+                        if (bb == wj) v = Rm[bb >> 1][bb & 1][idx];
+                    Rj[j][idx] = v;
+                }
+            } else {
+                const float* src = region(j, ((wj - j) & 3) - 1);
+#pragma unroll
+                for (int idx = 0; idx < 16; ++idx) Rj[j][idx] = src[idx * 64 + lane];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+                f32x4 v;
+#pragma unroll
+                for (int ee = 0; ee < 4; ++ee) {
+                    const int idx = 4 * q + ee;
+                    const float R0 = Rj[0][idx], R1 = Rj[1][idx], R2 = Rj[2][idx], R3 = Rj[3][idx];
+                    // j = 0, 1: R0 G[0] + R1 G[1];  j = 2, 3: R2 G[2] + R3 G[3]
+                    const float P0 = s == 0 ? R0 + 0.5f * R1 : 0.5f * R1;
+                    const float P1 = s == 0 ? 0.5f * R2 : s == 1 ? -0.5f * R2 : 0.5f * R2 + R3;
+                    v[ee] = P0 + P1;
+                }
+                const int k = (3 * r + s) * p.C + c_lo + cbo * 32 + 8 * q + 4 * lh;
+                *reinterpret_cast<f32x4*>(slab + (long long)n * p.Kcp + k) = v;
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    }
+}
+
 // ------------------------------------------------------- single-channel stem weight gradient
 // dW[n][tap] = sum_m dZ[m][n] x[m + tap] and db[n] = sum_m dZ[m][n] for the 1 -> N stem conv
 // (inc.c0): the layer is the read of dZ (N channels per pixel).  Blocks sweep 16 x 64 pixel tiles
@@ -1836,6 +2181,16 @@ static void plan_groups(WgradPlan* pl);
 // the Winograd-domain kernel: 3x3 / s1 / p1 on an even same-size grid, 64-channel input blocks
 // from one source each, 64-channel output blocks, the 6-product arithmetic, byte offsets of the
 // (shifted) sources and of dZ under 2^31; PU_WINO_WGRAD=0 keeps the direct kernels (A/B runs)
+// the Winograd weight gradient on one wave per SIMD (wgrad_wino4_x6_kernel, bit-identical):
+// PU_WW4=1 (A/B runs)
+static bool ww4_on() {
+    static const bool on = [] {
+        const char* e = getenv("PU_WW4");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 static bool wino_wgrad_ok(const pu_wgrad_args* a, const WgradPlan* pl) {
     static const bool on = [] {
         const char* e = getenv("PU_WINO_WGRAD");
@@ -2672,7 +3027,10 @@ extern "C" int pu_wgrad_phase(const pu_wgrad_args* a, void* workspace, size_t ws
             ww.x0_bytes = (unsigned)(px * a->c0 * 4);
             ww.x1_bytes = (unsigned)(px * a->c1 * 4);
             ww.p_bytes = (unsigned)((long long)pl.M * a->n * 4);
-            hipLaunchKernelGGL(wgrad_wino_x6_kernel, grid, dim3(512), 0, s, ww);
+            if (ww4_on() && (((uintptr_t)a->rows | (uintptr_t)a->src0 | (uintptr_t)a->src1) & 15) == 0)
+                hipLaunchKernelGGL(wgrad_wino4_x6_kernel, grid, dim3(256), 0, s, ww);
+            else
+                hipLaunchKernelGGL(wgrad_wino_x6_kernel, grid, dim3(512), 0, s, ww);
         } else if (pl.halo) {
             if (pl.nt == 2) hipLaunchKernelGGL(wgrad_halo_x6_kernel<2>, grid, dim3(512), 0, s, p);
             else hipLaunchKernelGGL(wgrad_halo_x6_kernel<1>, grid, dim3(256), 0, s, p);

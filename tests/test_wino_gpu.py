@@ -334,3 +334,45 @@ def test_wino4_bit_identical_to_8_wave_kernel(tmp_path):
                 assert (a is None) == (b is None), k
                 if a is not None:
                     assert torch.equal(a, b), (v, k, i, (a - b).abs().max().item())
+
+
+_WW4_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from punet import kernels as K, trunk as T
+out = {}
+for (B, H, W, c0, c1, N) in [(2, 16, 16, 64, 0, 64), (3, 10, 14, 128, 0, 128), (2, 8, 8, 64, 64, 64),
+                             (1, 32, 16, 128, 0, 192), (4, 8, 8, 512, 0, 512), (2, 16, 16, 256, 256, 256),
+                             (8, 64, 64, 64, 0, 64), (1, 2, 2, 64, 0, 64)]:
+    g = torch.Generator().manual_seed(B + H + W + c0 + c1 + N)
+    C = c0 + c1
+    x = torch.randn(B, H, W, C, generator=g).relu().cuda()
+    dz = (torch.randn(B, H, W, N, generator=g) * (torch.rand(B, H, W, N, generator=g) > 0.3).float()).cuda()
+    x0, x1 = (x[..., :c0].contiguous(), x[..., c0:].contiguous()) if c1 else (x, None)
+    dw, db = T.conv3x3_wgrad(dz, x0, x1)
+    out[(B, H, W, c0, c1, N)] = (dw.cpu(), db.cpu())
+torch.save(out, sys.argv[1])
+"""
+
+
+def test_wgrad_wino4_bit_identical_to_8_wave_kernel(tmp_path):
+    """wgrad_wino4_x6_kernel (one wave per SIMD, 2 x 2 channel blocks per position, 4-channel
+    producer threads, a 4-wave R exchange in the output transform; PU_WW4=1) and
+    wgrad_wino_x6_kernel form the same planes, run the same 6 products per accumulator in the same
+    order and the same G^T M G expression tree: weight and bias gradients bitwise equal - ragged
+    stages, concat sources, several channel blocks, split slabs, a single tile."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plastic-unet_amd")
+    res = {}
+    for on in ("1", "0"):
+        f = str(tmp_path / ("ww%s.pt" % on))
+        env = dict(os.environ, PU_WW4=on)
+        r = subprocess.run([sys.executable, "-c", _WW4_SCRIPT, f, root], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res[on] = torch.load(f, weights_only=True)
+    for k in res["1"]:
+        for i, (a, b) in enumerate(zip(res["1"][k], res["0"][k])):
+            assert torch.equal(a, b), (k, i, (a - b).abs().max().item())
