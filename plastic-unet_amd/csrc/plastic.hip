@@ -204,6 +204,16 @@ __device__ __forceinline__ f32x4 fh_ld4<__bf16>(const __bf16* p) {
     const b4 v = *reinterpret_cast<const b4*>(p);
     return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+// the pipelined head's feature stream: every feature is read once (row 0 aside), so the
+// nontemporal form (PU_HP_NT=1) keeps it from displacing H / w / alpha in the caches
+#ifndef PU_HP_NT
+#define PU_HP_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ f32x4 fh_ld4s(const T* p) {
+    if constexpr (PU_HP_NT && sizeof(T) == 4) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return fh_ld4<T>(p);
+}
 
 template <typename T, int L, int TPW, int R = FH_R>
 __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restrict__ feat, const float* __restrict__ wo,
@@ -408,9 +418,9 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
 //   waves 0..7 (streamers, the serial kernel's outconv configuration and per-CU stream rate): one
 //     continuous stream over the 17 rows in the order row 0, i0 .. i0+15, 256 pixels per pass with
 //     the next pass's loads issued before the current pass is reduced - so the block barriers
-//     between phases (every 2 passes = 4 rows) do not drain the memory pipeline;
+//     between phases (every 2 passes = 2 rows at U = 4) do not drain the memory pipeline;
 //   waves 8..11 (workers): phase 0 builds Weff = w + alpha (.) H_b in LDS; after every phase they
-//     form Y = X Weff for the 4 rows just streamed (thread = (column j, row pair), one k-ordered
+//     form Y = X Weff for the rows just streamed (thread = (column j, row), one k-ordered
 //     fmaf chain per row - the MFMA's chain, bit-identical), sigmoid, store; the phase after row 0's
 //     y0 runs the block's trace update.
 // What is left after the stream is one row's GEMM.  Arithmetic identical to head_fused_fwd_kernel
@@ -419,10 +429,10 @@ __global__ __launch_bounds__(FH_NT) void head_fused_fwd_kernel(const T* __restri
 #define PU_HP_SW 8
 #endif
 #ifndef PU_HP_ROT
-#define PU_HP_ROT 1
+#define PU_HP_ROT 0        // 1: per-block column rotation of the stream start (measured 2-4 % slower at U = 4)
 #endif
 #ifndef PU_HP_U
-#define PU_HP_U 8          // pixels in flight per streamer lane group and pass
+#define PU_HP_U 4          // pixels in flight per streamer lane group and pass (4: one row per pass)
 #endif
 constexpr int HP_SW = PU_HP_SW * 64, HP_NT = HP_SW + 256, HP_U = PU_HP_U, HP_N = 128;
 template <typename T>
@@ -439,7 +449,7 @@ __global__ __launch_bounds__(HP_NT) void head_pipe_fwd_kernel(const T* __restric
     constexpr int NPIX = (R + 1) * N;         // the stream: row 0, then rows i0 .. i0+15
     constexpr int NPASS = (NPIX + PPI - 1) / PPI;
     constexpr int NPH = (NPASS + 1) / 2;      // phases (2 passes each)
-    constexpr int RPP = 2 * PPI / N;          // stream rows per phase (4 with 8 streamer waves)
+    constexpr int RPP = 2 * PPI / N;          // stream rows per phase (2 with 8 streamer waves at U = 4)
     constexpr int RPT = RPP / 2;              // rows per worker thread and phase
     static_assert(PPI % N == 0 && RPT <= 3, "a pass is whole rows");
     static_assert(N / R == 8, "the XCD block order below assumes 8 row blocks per slot");
@@ -477,7 +487,7 @@ __global__ __launch_bounds__(HP_NT) void head_pipe_fwd_kernel(const T* __restric
                 const int q = min(k * PPI + tid / L + u * PPP, NPIX - 1);
                 const int r = q / N, col = (q + rot) & (N - 1);
                 const T* px = fb + ((long long)(r == 0 ? 0 : i0 + r - 1) * N + col) * C;
-                v[u] = fh_ld4<T>(px + lane * 4);
+                v[u] = fh_ld4s<T>(px + lane * 4);
             }
         };
         const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + lane * 4);
@@ -503,7 +513,7 @@ __global__ __launch_bounds__(HP_NT) void head_pipe_fwd_kernel(const T* __restric
                 if (lane == 0 && q < NPIX) xs[(q & ~(N - 1)) + ((q + rot) & (N - 1))] = t + bias;
             }
         };
-        // passes in pairs (static buffer roles): a phase = 2 passes = 4 rows, then the barrier
+        // passes in pairs (static buffer roles): a phase = 2 passes = 2 rows, then the barrier
         load(0, buf[0]);
 #pragma unroll 1
         for (int k = 0; k < NPASS; k += 2) {
