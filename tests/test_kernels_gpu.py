@@ -241,7 +241,8 @@ def test_maxpool(B, H, W, C):
     assert torch.equal(nchw(dxk2).cpu(), xr.grad)
 
 
-@pytest.mark.parametrize("rows_hw,C", [((2, 16, 16), 64), ((1, 8, 8), 8), ((3, 5, 7), 128)])
+@pytest.mark.parametrize("rows_hw,C", [((2, 16, 16), 64), ((1, 8, 8), 8), ((3, 5, 7), 128), ((2, 9, 13), 16),
+                                         ((2, 17, 11), 32), ((4, 96, 96), 8), ((2, 64, 64), 32)])
 def test_outconv(rows_hw, C):
     B, H, W = rows_hw
     g = torch.Generator().manual_seed(C + H)

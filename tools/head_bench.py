@@ -1,6 +1,7 @@
 """Fused plastic head forward (pu_plastic_head_fwd) at bs 32 x 128^2, C = 64: us per launch and
 algorithmic GB/s (the bench line's oja_update.fused_head_bs32), for the library PLASTIC_UNET_LIB
-points at (ablation variants).   python tools/head_bench.py [label]"""
+points at (ablation variants).   python tools/head_bench.py [label] [B N C]  (default 32 128 64 = C2;
+32 256 8 = C4)"""
 import os
 import sys
 
@@ -12,7 +13,7 @@ from punet import kernels as K  # noqa: E402
 import bench  # noqa: E402
 
 dev = torch.device("cuda", 0)
-B, N, C = 32, 128, 64
+B, N, C = (int(v) for v in sys.argv[2:5]) if len(sys.argv) >= 5 else (32, 128, 64)
 torch.manual_seed(0)
 H = 0.1 * torch.randn(B, N, N, device=dev)
 w = 0.01 * torch.randn(N, N, device=dev)
