@@ -2799,6 +2799,22 @@ __global__ __launch_bounds__(256) void wgrad_reduce_wide_kernel(const float* __r
 
 // phase 2 of every weight-gradient path: fixed-order fp64 reduction of the split partials and
 // the scatter into PyTorch's [n][c][kh][kw] (+ bias)
+// The one-launch wide reduction also takes the non-Winograd plans whose slab rows are short
+// (Nr x Kcp <= WR_WIDE_MAX entries: C4 / C5's 32-channel weight gradients, 9216 entries over
+// hundreds of splits), where the grouped form is two latency-bound launches: C5 +0.8 %, C4 +0.7 %
+// (`r06_experiments/wgrad_reduce_wide_ab.txt`).  Long rows (C2 / C3, >= 32K entries) keep the
+// grouped form: the wide one took C3's bf16 reductions from 0.36 to 1.39 ms per step.
+// PU_WR_WIDE (A/B runs): 0 = small / stem / pointwise plans only (the round-6 form), 2 = every plan.
+// The split partials are summed in fp64 either way, in a different fixed order.
+constexpr long long WR_WIDE_MAX = 16384;
+static int wr_wide_mode() {
+    static const int m = [] {
+        const char* e = getenv("PU_WR_WIDE");
+        return e ? atoi(e) : 1;
+    }();
+    return m;
+}
+
 static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* workspace, hipStream_t s) {
     const long long total = (long long)pl.Nr * pl.Kcp;
     const long long threads = total + (a->bias_mode == 2 ? pl.C : 0);
@@ -2807,7 +2823,9 @@ static int wgrad_reduce(const WgradPlan& pl, const pu_wgrad_args* a, void* works
     // one launch for up to 1024 splits of a few-thousand-entry slab (the direct small-channel /
     // stem kernels; measured slower than the two-pass grouped form on the Winograd-domain
     // kernel's 64-256 splits: 0.37 vs 0.32 ms per C2 step)
-    if ((pl.small || pl.stem || pl.pw) && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
+    const bool wide = pl.small || pl.stem || pl.pw || (wr_wide_mode() == 1 && !pl.wino && total <= WR_WIDE_MAX) ||
+                      wr_wide_mode() == 2;
+    if (wide && a->bias_mode != 2 && pl.Kcp % 4 == 0) {
         hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)ceil_div(total, (long long)WR_E)), dim3(256), 0, s,
                            (const float*)workspace, pl.splits, total, a->n, pl.Kcp, pl.K, pl.C, a->kh, a->kw,
                            a->bias_mode, a->dweight, a->dbias, a->accumulate);
