@@ -621,26 +621,42 @@ __global__ __launch_bounds__(256) void head_dx_kernel(const float* __restrict__ 
     const long long off = (long long)b * N * N;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     float acc[M][M] = {};
-    for (int j0 = 0; j0 < N; j0 += HK) {
-        for (int e = threadIdx.x; e < HK * T; e += 256) {
-            int jj = e % HK, rr = e / HK;
-            int gj = j0 + jj;
-            int gi = i0 + rr;
-            float g = 0.f;
+    // the next chunk's operands are loaded into registers before this chunk's FMAs (raw values;
+    // out-of-range entries load as 0, which the expressions below map to the 0 the tile needs)
+    constexpr int E = HK * T / 256;
+    static_assert(HK * T % 256 == 0, "whole loader rounds");
+    float rdy[E], ryv[E], rw[E], ra[E], rh[E];
+    auto fetch = [&](int j0) {
+#pragma unroll
+        for (int u = 0; u < E; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            const int jj = e % HK, rr = e / HK;
+            const int gj = j0 + jj, gi = i0 + rr, gk = k0 + rr;
+            rdy[u] = ryv[u] = rw[u] = ra[u] = rh[u] = 0.f;
             if (gi < N && gj < N) {
-                long long o = off + (long long)gi * N + gj;
-                g = sig_bwd(dY[o], Yv[o]);
+                const long long o = off + (long long)gi * N + gj;
+                rdy[u] = dY[o];
+                ryv[u] = Yv[o];
             }
-            gs[jj][rr] = g;
-            int gk = k0 + rr;
-            float v = 0.f;
             if (gk < N && gj < N) {
-                long long o = (long long)gk * N + gj;
-                v = w[o] + alpha[o] * H[off + o];
+                const long long o = (long long)gk * N + gj;
+                rw[u] = w[o];
+                ra[u] = alpha[o];
+                rh[u] = H[off + o];
             }
-            ws[jj][rr] = v;
+        }
+    };
+    fetch(0);
+    for (int j0 = 0; j0 < N; j0 += HK) {
+#pragma unroll
+        for (int u = 0; u < E; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            const int jj = e % HK, rr = e / HK;
+            gs[jj][rr] = sig_bwd(rdy[u], ryv[u]);
+            ws[jj][rr] = rw[u] + ra[u] * rh[u];
         }
         __syncthreads();
+        if (j0 + HK < N) fetch(j0 + HK);
 #pragma unroll
         for (int jj = 0; jj < HK; ++jj) {
             float a[M], bb[M];
@@ -680,20 +696,36 @@ __global__ __launch_bounds__(256) void head_dw_kernel(const float* __restrict__ 
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const long long off = (long long)b * N * N;
     float t[M][M] = {};
-    for (int i0 = 0; i0 < N; i0 += HK) {
-        for (int e = threadIdx.x; e < HK * T; e += 256) {
-            int cc = e % T, ii = e / T;
-            int gi = i0 + ii;
-            int gk = k0 + cc, gj = j0 + cc;
-            xs[ii][cc] = (gi < N && gk < N) ? X[off + (long long)gi * N + gk] : 0.f;
-            float g = 0.f;
+    // next chunk's raw operands in registers during this chunk's FMAs (as head_dx_kernel)
+    constexpr int E = HK * T / 256;
+    static_assert(HK * T % 256 == 0, "whole loader rounds");
+    float rx[E], rdy[E], ryv[E];
+    auto fetch = [&](int i0) {
+#pragma unroll
+        for (int u = 0; u < E; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            const int cc = e % T, ii = e / T;
+            const int gi = i0 + ii, gk = k0 + cc, gj = j0 + cc;
+            rx[u] = (gi < N && gk < N) ? X[off + (long long)gi * N + gk] : 0.f;
+            rdy[u] = ryv[u] = 0.f;
             if (gi < N && gj < N) {
-                long long o = off + (long long)gi * N + gj;
-                g = sig_bwd(dY[o], Yv[o]);
+                const long long o = off + (long long)gi * N + gj;
+                rdy[u] = dY[o];
+                ryv[u] = Yv[o];
             }
-            gs[ii][cc] = g;
+        }
+    };
+    fetch(0);
+    for (int i0 = 0; i0 < N; i0 += HK) {
+#pragma unroll
+        for (int u = 0; u < E; ++u) {
+            const int e = threadIdx.x + 256 * u;
+            const int cc = e % T, ii = e / T;
+            xs[ii][cc] = rx[u];
+            gs[ii][cc] = sig_bwd(rdy[u], ryv[u]);
         }
         __syncthreads();
+        if (i0 + HK < N) fetch(i0 + HK);
 #pragma unroll
         for (int ii = 0; ii < HK; ++ii) {
             float a[M], bb[M];
